@@ -1,0 +1,128 @@
+/*
+ * rs_mi355x.h — C-ABI of the MI355X-native Leopard-FFT Reed-Solomon engine.
+ *
+ * This is the drop-in boundary for the hot path of bpfs/reedsolomon16: the
+ * Go methods leopardFF16/leopardFF8 {Encode, Verify, Reconstruct,
+ * ReconstructData, ReconstructSome} are replaced by calls into this library
+ * through a thin cgo shim.  Every entry point cites the
+ * reference interface it replaces.  Plain pointers and sizes only; no torch
+ * or HIP types appear in the signatures (a stream is passed as void*).
+ *
+ * Shard model (identical to the Go [][]byte model):
+ *   shards[0..k)   data shards,  shards[k..k+p) parity shards;
+ *   lens[i]        length of shard i; 0 means "missing" (Go: len(shards[i])==0).
+ * Encode/Verify require every len equal (checkShards(shards,false),
+ * encoder.go:102-115) and a multiple of 64 (leopard16.go:130).
+ * GF(2^16) symbol layout: each 64-byte block holds 32 symbols, low bytes in
+ * [0,32) and high bytes in [32,64) (leopard16.go:778-792).
+ *
+ * All calls are thread-safe (one mutex per codec, like the Go encoder's
+ * sync.Pool/sync.Once design allows concurrent callers, leopard16.go:25).
+ */
+#ifndef RS_MI355X_H
+#define RS_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes: 1:1 with the reference's sentinel errors (reedsolomon.go:15-33). */
+#define RS_OK                       0
+#define RS_ERR_INV_SHARD_NUM        1  /* ErrInvShardNum        reedsolomon.go:16 */
+#define RS_ERR_MAX_SHARD_NUM        2  /* ErrMaxShardNum        reedsolomon.go:17 */
+#define RS_ERR_TOO_FEW_SHARDS       3  /* ErrTooFewShards       reedsolomon.go:18 */
+#define RS_ERR_SHARD_NO_DATA        4  /* ErrShardNoData        reedsolomon.go:19 */
+#define RS_ERR_SHARD_SIZE           5  /* ErrShardSize          reedsolomon.go:20 */
+#define RS_ERR_INVALID_SHARD_SIZE   6  /* ErrInvalidShardSize   reedsolomon.go:25 */
+#define RS_ERR_NOT_SUPPORTED        7  /* ErrNotSupported       reedsolomon.go:27 */
+#define RS_ERR_SHORT_DATA           8  /* ErrShortData          reedsolomon.go:26 */
+#define RS_ERR_RECONSTRUCT_REQUIRED 9  /* ErrReconstructRequired reedsolomon.go:24 */
+/* Conditions that have no sentinel in the reference: */
+#define RS_ERR_PANIC               50  /* the Go code panics (slice index out of range) for this geometry */
+#define RS_ERR_NOMEM               51  /* host or device allocation failed */
+#define RS_ERR_DEVICE              52  /* HIP runtime / kernel launch failure */
+#define RS_ERR_INVALID_ARG         53  /* NULL codec / pointer arguments */
+
+typedef struct rs_codec rs_codec;
+
+/* Construction.  field_bits: 16 -> New16 (reedsolomon.go:90-93, newFF16
+ * leopard16.go:36-54); 8 -> New8 (reedsolomon.go:84-87, newFF8
+ * leopard8.go:53-75); 0 -> New (reedsolomon.go:69-81: GF(2^8) iff k+p<=256).
+ * device: HIP device ordinal the codec's kernels run on.
+ * Returns RS_ERR_INV_SHARD_NUM / RS_ERR_MAX_SHARD_NUM like the Go constructors. */
+int rs_new(int field_bits, int data_shards, int parity_shards, int device, rs_codec **out);
+void rs_free(rs_codec *codec);
+
+/* Extensions interface (reedsolomon.go:358-375). */
+int rs_field_bits(const rs_codec *codec);
+int rs_data_shards(const rs_codec *codec);
+int rs_parity_shards(const rs_codec *codec);
+int rs_total_shards(const rs_codec *codec);
+int rs_shard_size_multiple(const rs_codec *codec); /* 64: leopard16.go:58-60 */
+
+/* ---------------- Host-memory entry points (Go [][]byte semantics) ---------------- */
+
+/* Encode: leopardFF16.Encode leopard16.go:116-125 / leopardFF8.Encode
+ * leopard8.go:141-150.  Writes parity into shards[k..k+p). */
+int rs_encode(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards);
+
+/* Verify: leopard16.go:361-387 / leopard8.go:415-436.  *ok = 1 iff parity matches. */
+int rs_verify(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards, int *ok);
+
+/* Reconstruct / ReconstructData / ReconstructSome: leopard16.go:343-358
+ * (reconstruct :390-570), leopard8.go:392-407 (reconstruct :439-695).
+ * recover_all = 1 (Reconstruct, or ReconstructSome with len(required)==total)
+ * or 0 (ReconstructData).  Missing shards have lens[i]==0; for each one that
+ * is rebuilt, shards[i] must point at >= S writable bytes (the cgo shim does
+ * the Go slice resize, :556-560) and lens[i] is set to S on return. */
+int rs_reconstruct(rs_codec *codec, uint8_t *const *shards, size_t *lens, int nshards, int recover_all);
+
+/* EncodeIdx / Update: return RS_ERR_NOT_SUPPORTED (leopard16.go:227-229, 273-275). */
+int rs_encode_idx(rs_codec *codec, const uint8_t *data_shard, size_t len, int idx, uint8_t *const *parity,
+                  const size_t *parity_lens, int nparity);
+int rs_update(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards,
+              uint8_t *const *new_data, const size_t *new_lens, int nnew);
+
+/* ---------------- Device-resident entry points (HBM in, HBM out) ---------------- */
+/* d_shards: HOST array of k+p DEVICE pointers, each to shard_size bytes
+ * (4-byte aligned; 64-byte aligned recommended).  stream: hipStream_t or NULL
+ * for the codec's own stream.  rs_encode_dev is asynchronous on `stream` when
+ * the rows are equally strided (the common AllocAligned slab layout); the
+ * other calls return after their work is complete. */
+int rs_encode_dev(rs_codec *codec, uint8_t *const *d_shards, size_t shard_size, void *stream);
+int rs_verify_dev(rs_codec *codec, uint8_t *const *d_shards, size_t shard_size, int *ok, void *stream);
+/* present[i] != 0 marks shard i present; rebuilt rows are written into d_shards[i]. */
+int rs_reconstruct_dev(rs_codec *codec, uint8_t *const *d_shards, const uint8_t *present, size_t shard_size,
+                       int recover_all, void *stream);
+
+/* Batched device encode of `nstripes` independent stripes laid out as one slab
+ * per stripe: stripe j, shard i at d_base + j*stripe_stride + i*row_stride.
+ * Asynchronous on `stream`. */
+int rs_encode_dev_batch(rs_codec *codec, uint8_t *d_base, size_t row_stride, size_t stripe_stride,
+                        int nstripes, size_t shard_size, void *stream);
+
+/* Name of the kernel path the codec uses for encode ("reg-m32", "lds", "multipass", ...). */
+const char *rs_encode_path(const rs_codec *codec);
+
+/* ---------------- Host-only diagnostics (no device calls; used by CPU tests) ---------------- */
+/* Field tables as built by the engine (initLUTs/initFFTSkew, leopard16.go:940-1031). */
+int rs_debug_field_tables(int field_bits, uint16_t *log_out, uint16_t *exp_out, uint16_t *skew_out,
+                          uint16_t *walsh_out);
+/* Byte-permute twiddle image of "multiply by exp(log_m)" (rs_debug_twiddle_dwords() dwords). */
+int rs_debug_twiddle(int field_bits, uint32_t log_m, uint32_t *out);
+int rs_debug_twiddle_dwords(int field_bits);
+/* Error locators for an erasure pattern (leopard16.go:433-470); out has 2^field_bits entries.
+ * Returns RS_ERR_PANIC where the reference panics. */
+int rs_debug_error_locators(int field_bits, int data_shards, int parity_shards, const uint8_t *erased,
+                            uint32_t *out);
+
+/* Human-readable message for an error code. */
+const char *rs_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RS_MI355X_H */

@@ -1,0 +1,318 @@
+"""Python mirror of the reference's ``ReedSolomon`` codec interface for the hot
+path (bpfs/reedsolomon16 reedsolomon.go:37-93, leopard16.go:36-387,
+leopard8.go:53-436), running on the MI355X engine through the C-ABI.
+
+Names, argument meaning and error behaviour follow the Go API:
+
+* ``New(k, p)`` picks GF(2^8) when k+p <= 256, else GF(2^16) (reedsolomon.go:69-81);
+  ``New8`` / ``New16`` force the field.
+* ``encode(shards)`` fills ``shards[k:]`` in place; ``verify`` returns bool;
+  ``reconstruct`` / ``reconstruct_data`` / ``reconstruct_some`` replace missing
+  entries (``None`` or empty) with rebuilt arrays, like the Go slice resize.
+* Errors raise the sentinel exception classes below (``ErrTooFewShards`` ...).
+
+Host shards are numpy ``uint8`` arrays.  Device-resident variants take torch
+CUDA tensors (one per shard, or a 2-D ``[k+p, S]`` tensor) and run on the
+current torch stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import io
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _capi
+
+
+# --------------------------------------------------------------------------- errors
+class RSError(Exception):
+    code = -1
+
+
+def _mk(name: str, code: int, doc: str):
+    cls = type(name, (RSError,), {"code": code, "__doc__": doc})
+    globals()[name] = cls
+    return cls
+
+
+_ERRORS = {
+    1: _mk("ErrInvShardNum", 1, "reedsolomon.go:16"),
+    2: _mk("ErrMaxShardNum", 2, "reedsolomon.go:17"),
+    3: _mk("ErrTooFewShards", 3, "reedsolomon.go:18"),
+    4: _mk("ErrShardNoData", 4, "reedsolomon.go:19"),
+    5: _mk("ErrShardSize", 5, "reedsolomon.go:20"),
+    6: _mk("ErrInvalidShardSize", 6, "reedsolomon.go:25"),
+    7: _mk("ErrNotSupported", 7, "reedsolomon.go:27"),
+    8: _mk("ErrShortData", 8, "reedsolomon.go:26"),
+    9: _mk("ErrReconstructRequired", 9, "reedsolomon.go:24"),
+    50: _mk("ErrPanic", 50, "the Go reference panics (index out of range) for this geometry"),
+    51: _mk("ErrNoMem", 51, "allocation failed"),
+    52: _mk("ErrDevice", 52, "HIP device error"),
+    53: _mk("ErrInvalidArg", 53, "invalid argument"),
+}
+ErrInvShardNum = _ERRORS[1]
+ErrMaxShardNum = _ERRORS[2]
+ErrTooFewShards = _ERRORS[3]
+ErrShardNoData = _ERRORS[4]
+ErrShardSize = _ERRORS[5]
+ErrInvalidShardSize = _ERRORS[6]
+ErrNotSupported = _ERRORS[7]
+ErrShortData = _ERRORS[8]
+ErrReconstructRequired = _ERRORS[9]
+ErrPanic = _ERRORS[50]
+ErrDevice = _ERRORS[52]
+
+
+def _check(code: int) -> None:
+    if code != 0:
+        cls = _ERRORS.get(code, RSError)
+        raise cls(_capi.lib().rs_strerror(code).decode())
+
+
+# --------------------------------------------------------------------------- helpers
+def _host_rows(shards: Sequence):
+    n = len(shards)
+    ptrs = (C.c_void_p * n)()
+    lens = (C.c_size_t * n)()
+    keep = []
+    for i, s in enumerate(shards):
+        if s is None or len(s) == 0:
+            ptrs[i] = None
+            lens[i] = 0
+            continue
+        a = np.asarray(s)
+        if a.dtype != np.uint8 or not a.flags["C_CONTIGUOUS"]:
+            raise TypeError("host shards must be C-contiguous numpy uint8 arrays")
+        keep.append(a)
+        ptrs[i] = a.ctypes.data
+        lens[i] = a.nbytes
+    return ptrs, lens, keep
+
+
+def _dev_rows(rows, total: int):
+    """torch CUDA tensors -> (ptr array, shard size)."""
+    if hasattr(rows, "dim") and rows.dim() == 2:
+        rows = [rows[i] for i in range(rows.shape[0])]
+    if len(rows) != total:
+        raise ErrTooFewShards("need %d shards, got %d" % (total, len(rows)))
+    ptrs = (C.c_void_p * total)()
+    S = None
+    for i, t in enumerate(rows):
+        if t is None:
+            ptrs[i] = None
+            continue
+        if not t.is_cuda or t.dtype.itemsize != 1 or not t.is_contiguous():
+            raise TypeError("device shards must be contiguous uint8 CUDA tensors")
+        ptrs[i] = t.data_ptr()
+        S = t.numel() if S is None else S
+    return ptrs, S or 0
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+
+        return torch.cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+# --------------------------------------------------------------------------- codec
+class ReedSolomon:
+    """One encoder instance (leopardFF16 / leopardFF8 behind the ReedSolomon interface)."""
+
+    def __init__(self, data_shards: int, parity_shards: int, field_bits: int = 0, device: Optional[int] = None):
+        L = _capi.lib()
+        if device is None:
+            device = 0
+            try:
+                import torch
+
+                if torch.cuda.is_available():
+                    device = torch.cuda.current_device()
+            except Exception:
+                pass
+        h = C.c_void_p()
+        _check(L.rs_new(field_bits, data_shards, parity_shards, device, C.byref(h)))
+        self._h = h
+        self._L = L
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.rs_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # Extensions (reedsolomon.go:358-375)
+    def data_shards(self) -> int:
+        return self._L.rs_data_shards(self._h)
+
+    def parity_shards(self) -> int:
+        return self._L.rs_parity_shards(self._h)
+
+    def total_shards(self) -> int:
+        return self._L.rs_total_shards(self._h)
+
+    def shard_size_multiple(self) -> int:
+        return self._L.rs_shard_size_multiple(self._h)
+
+    @property
+    def field_bits(self) -> int:
+        return self._L.rs_field_bits(self._h)
+
+    @property
+    def encode_path(self) -> str:
+        return self._L.rs_encode_path(self._h).decode()
+
+    def alloc_aligned(self, each: int, shards: Optional[int] = None):
+        """AllocAligned (unsafe.go:17-41): one 64-byte-aligned slab, rows of `each` bytes."""
+        n = self.total_shards() if shards is None else shards
+        each_al = (each + 63) // 64 * 64
+        raw = np.zeros(each_al * n + 64, dtype=np.uint8)
+        off = (-raw.ctypes.data) % 64
+        slab = raw[off:off + each_al * n]
+        return [slab[i * each_al:i * each_al + each] for i in range(n)]
+
+    # ---------------- host-memory operations (Go [][]byte semantics)
+    def encode(self, shards: list) -> None:
+        """Encode (leopard16.go:116-125): parity written into shards[k:]."""
+        ptrs, lens, _keep = _host_rows(shards)
+        _check(self._L.rs_encode(self._h, ptrs, lens, len(shards)))
+
+    def verify(self, shards: list) -> bool:
+        """Verify (leopard16.go:361-387)."""
+        ptrs, lens, _keep = _host_rows(shards)
+        ok = C.c_int(0)
+        _check(self._L.rs_verify(self._h, ptrs, lens, len(shards), C.byref(ok)))
+        return bool(ok.value)
+
+    def _reconstruct(self, shards: list, recover_all: bool) -> list:
+        total = len(shards)
+        S = next((len(s) for s in shards if s is not None and len(s)), 0)
+        k = self.data_shards()
+        end = total if recover_all else min(k, total)
+        bufs = list(shards)
+        for i in range(min(end, total)):
+            if bufs[i] is None or len(bufs[i]) == 0:
+                bufs[i] = np.zeros(S, dtype=np.uint8)  # Go: make([]byte, shardSize)
+        ptrs = (C.c_void_p * total)()
+        lens = (C.c_size_t * total)()
+        for i, s in enumerate(shards):
+            present = s is not None and len(s) > 0
+            b = bufs[i]
+            if b is not None and len(b):
+                b = np.asarray(b)
+                if b.dtype != np.uint8 or not b.flags["C_CONTIGUOUS"]:
+                    raise TypeError("host shards must be C-contiguous numpy uint8 arrays")
+                bufs[i] = b
+                ptrs[i] = b.ctypes.data
+            lens[i] = len(s) if present else 0
+        _check(self._L.rs_reconstruct(self._h, ptrs, lens, total, int(recover_all)))
+        for i in range(total):
+            if lens[i] and (shards[i] is None or len(shards[i]) == 0):
+                shards[i] = bufs[i]
+        return shards
+
+    def reconstruct(self, shards: list) -> list:
+        """Reconstruct (leopard16.go:351-353): rebuild every missing shard."""
+        return self._reconstruct(shards, True)
+
+    def reconstruct_data(self, shards: list) -> list:
+        """ReconstructData (leopard16.go:356-358): rebuild missing data shards only."""
+        return self._reconstruct(shards, False)
+
+    def reconstruct_some(self, shards: list, required: Sequence[bool]) -> list:
+        """ReconstructSome (leopard16.go:343-348): only len(required) matters."""
+        return self._reconstruct(shards, len(required) == self.total_shards())
+
+    def encode_idx(self, data_shard, idx: int, parity: list) -> None:
+        """EncodeIdx (leopard16.go:227-229): not supported."""
+        _check(self._L.rs_encode_idx(self._h, None, 0, idx, None, None, 0))
+
+    def update(self, shards: list, new_datashards: list) -> None:
+        """Update (leopard16.go:273-275): not supported."""
+        _check(self._L.rs_update(self._h, None, None, 0, None, None, 0))
+
+    # ---------------- Split / Join (leopard16.go:232-340): host byte layout either side of the codec
+    def split(self, data) -> list:
+        data = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        if len(data) == 0:
+            raise ErrShortData("not enough data to fill the number of requested shards")
+        k, total = self.data_shards(), self.total_shards()
+        if total == 1 and len(data) & 63 == 0:
+            return [data]
+        per = (len(data) + k - 1) // k
+        per = (per + 63) // 64 * 64
+        buf = np.zeros(total * per, dtype=np.uint8)
+        buf[:len(data)] = data
+        return [buf[i * per:(i + 1) * per] for i in range(total)]
+
+    def join(self, dst, shards: list, out_size: int) -> None:
+        k = self.data_shards()
+        if len(shards) < k:
+            raise ErrTooFewShards("too few shards given")
+        shards = shards[:k]
+        size = 0
+        for s in shards:
+            if s is None:
+                raise ErrReconstructRequired("reconstruction required as one or more required data shards are nil")
+            size += len(s)
+            if size >= out_size:
+                break
+        if size < out_size:
+            raise ErrShortData("not enough data to fill the number of requested shards")
+        write = out_size
+        for s in shards:
+            if write < len(s):
+                dst.write(bytes(np.asarray(s)[:write]))
+                return
+            dst.write(bytes(np.asarray(s)))
+            write -= len(s)
+
+    # ---------------- device-resident operations (torch CUDA tensors)
+    def encode_dev(self, rows, stream=None) -> None:
+        """Encode shards already in HBM; asynchronous on `stream` (default: current torch stream)."""
+        ptrs, S = _dev_rows(rows, self.total_shards())
+        _check(self._L.rs_encode_dev(self._h, ptrs, S, _stream_handle(stream)))
+
+    def verify_dev(self, rows, stream=None) -> bool:
+        ptrs, S = _dev_rows(rows, self.total_shards())
+        ok = C.c_int(0)
+        _check(self._L.rs_verify_dev(self._h, ptrs, S, C.byref(ok), _stream_handle(stream)))
+        return bool(ok.value)
+
+    def reconstruct_dev(self, rows, present: Sequence[bool], recover_all: bool = True, stream=None) -> None:
+        """Rebuild rows whose `present` flag is False, in place in HBM."""
+        ptrs, S = _dev_rows(rows, self.total_shards())
+        pr = (C.c_uint8 * self.total_shards())(*[1 if x else 0 for x in present])
+        _check(self._L.rs_reconstruct_dev(self._h, ptrs, pr, S, int(recover_all), _stream_handle(stream)))
+
+    def encode_dev_batch(self, slab, stream=None) -> None:
+        """Encode a [nstripes, k+p, S] uint8 CUDA tensor (one launch for all stripes)."""
+        if slab.dim() != 3 or slab.shape[1] != self.total_shards() or not slab.is_contiguous():
+            raise TypeError("slab must be a contiguous [nstripes, k+p, S] uint8 CUDA tensor")
+        n, _, S = slab.shape
+        _check(self._L.rs_encode_dev_batch(self._h, slab.data_ptr(), S, slab.stride(0), n, S,
+                                           _stream_handle(stream)))
+
+
+def New(data_shards: int, parity_shards: int, device: Optional[int] = None) -> ReedSolomon:
+    """New (reedsolomon.go:69-81): GF(2^8) when data+parity <= 256, else GF(2^16)."""
+    return ReedSolomon(data_shards, parity_shards, 0, device)
+
+
+def New8(data_shards: int, parity_shards: int, device: Optional[int] = None) -> ReedSolomon:
+    """New8 (reedsolomon.go:84-87)."""
+    return ReedSolomon(data_shards, parity_shards, 8, device)
+
+
+def New16(data_shards: int, parity_shards: int, device: Optional[int] = None) -> ReedSolomon:
+    """New16 (reedsolomon.go:90-93)."""
+    return ReedSolomon(data_shards, parity_shards, 16, device)

@@ -1,0 +1,80 @@
+// Host-side finite-field tables and GPU twiddle-table construction.
+//
+// Field construction follows the reference exactly:
+//   GF(2^16): initLUTs / initFFTSkew  leopard16.go:940-1031 (poly 0x1002D, Cantor basis)
+//   GF(2^8):  initLUTs8 / initFFTSkew8 leopard8.go:1034-1122 (poly 0x11D)
+// The GPU never sees log/exp tables: every multiply by a constant (a "twiddle",
+// given as its log) is shipped as a small set of byte-permute tables that the
+// kernels evaluate with v_perm_b32 (see kernels.hip, mul_add).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace rs {
+
+constexpr int kTwDwords16 = 24;  // per-twiddle table size in dwords (GF(2^16))
+constexpr int kTwDwords8 = 8;    // per-twiddle table size in dwords (GF(2^8))
+
+struct Field {
+    int bits = 0;       // 8 or 16
+    uint32_t order = 0; // 2^bits
+    uint32_t mod = 0;   // 2^bits - 1 ("modulus": a log value meaning "multiply by zero")
+    std::vector<uint16_t> log, exp, skew, walsh;
+
+    uint32_t add_mod(uint32_t a, uint32_t b) const {  // leopard16.go:840-845
+        uint32_t s = a + b;
+        return (s + (s >> bits)) & mod;
+    }
+    uint32_t sub_mod(uint32_t a, uint32_t b) const {  // leopard16.go:847-851
+        uint32_t d = a - b;
+        return (d + (d >> bits)) & mod;
+    }
+    uint32_t mul_log(uint32_t a, uint32_t log_b) const {  // leopard16.go:828-838
+        if (a == 0) return 0;
+        return exp[add_mod(log[a], log_b)];
+    }
+    void fwht(uint32_t *data, int mtrunc) const;  // leopard16.go:865-900
+};
+
+const Field &field(int bits);  // built once, thread-safe
+
+// Perm-table image of "multiply by exp(log_m)" for the GPU (kTwDwords* dwords).
+void make_twiddle(const Field &F, uint32_t log_m, uint32_t *out);
+inline int tw_dwords(int bits) { return bits == 16 ? kTwDwords16 : kTwDwords8; }
+
+inline int ceil_pow2(int n) { return n <= 1 ? 1 : 1 << (64 - __builtin_clzll((unsigned long long)(n - 1))); }
+inline int ilog2(int n) { return 31 - __builtin_clz((unsigned)n); }
+
+// Twiddle slot schedules.  A transform of size M = 2^L is a sequence of
+// passes; radix-4 passes hold 3 slots per butterfly group in the order
+// (m01, m02, m23); the radix-2 pass of an odd L holds 1 slot (IFFT) or one
+// slot per row pair (FFT).  Kernels and host use the same offsets.
+struct PassInfo {
+    int dist;      // butterfly distance
+    int radix;     // 4 or 2
+    int groups;    // butterfly groups in the pass (radix-4: M/(4*dist); radix-2 IFFT: 1; radix-2 FFT: M/2)
+    int slot_off;  // first slot of the pass
+};
+std::vector<PassInfo> ifft_passes(int logm);  // dist = 1, 4, 16, ... then radix-2 at M/2
+std::vector<PassInfo> fft_passes(int logm);   // dist = M/4, M/16, ... then radix-2 at 1
+int ifft_slots(int logm);
+int fft_slots(int logm);
+
+// Twiddle LOG values for the reference's encode schedule (leopard16.go:128-224):
+// chunk c's IFFT (skew base m-1+c*m, indices skewLUT[iend], [iend+dist],
+// [iend+2*dist], radix-2 [dist]) and the final FFT (fftSkew[iEnd-1]...).
+// Groups the reference skips (r >= mtrunc) get `mod` (they act on zero rows).
+// Returns false when the reference would panic (skew index out of range).
+bool encode_schedule(const Field &F, int k, int p, std::vector<uint32_t> &ifft_logs, std::vector<uint32_t> &fft_logs,
+                     int &nchunks);
+
+// Decoder schedules over n = ceilPow2(m+k) rows (leopard16.go:573-657).
+bool decode_schedule(const Field &F, int k, int p, std::vector<uint32_t> &ifft_logs, std::vector<uint32_t> &fft_logs);
+
+// Error locators (log domain) for an erasure pattern, leopard16.go:433-470
+// (GF(2^8): leopard8.go:478-531).  erased[i] for i in [0, k+p), data first.
+// Returns false when the reference would panic (GF(2^8) with m+k > 256).
+bool error_locators(const Field &F, int k, int p, const uint8_t *erased, std::vector<uint32_t> &err_locs);
+
+}  // namespace rs

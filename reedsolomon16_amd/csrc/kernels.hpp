@@ -1,0 +1,59 @@
+// Launcher interface between the host codec (codec.cpp) and the HIP kernels
+// (kernels.hip).  Only plain pointers and sizes cross this boundary.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace rs {
+
+// A set of shard rows in device memory: either an explicit device array of
+// row pointers, or base + i*stride.
+struct RowSet {
+    uint8_t *const *table;  // device array (nullable)
+    uint8_t *base;
+    uint64_t stride;
+};
+
+// Fused register-resident encode (m <= 32): one lane owns a column unit of
+// every row; chunked IFFT + XOR-accumulate + FFT stay in VGPRs.
+struct EncodeArgs {
+    RowSet data;            // k rows
+    RowSet parity;          // p rows
+    int k, p, nchunks;
+    uint64_t shard_size;    // bytes per row
+    uint64_t stripe_stride; // batched: byte offset between stripes (applied to both RowSets' base)
+    int nstripes;
+    const uint32_t *tw_ifft;  // nchunks * ifft_slots(logm) twiddle tables
+    const uint32_t *tw_fft;   // fft_slots(logm) twiddle tables
+    int *mismatch;            // verify: set to 1 on any parity mismatch
+};
+
+// Returns hipSuccess or the launch error.  logm in [0, 5].
+hipError_t launch_encode_reg(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
+// Name of the register-kernel variant (for diagnostics / profiles).
+const char *encode_reg_name(int bits, int logm);
+
+// ---- Multi-pass building blocks (any m / n; work rows contiguous, stride = shard_size) ----
+// work[dst0 + r] = r < cnt ? src.row(row0 + r) : 0, for r in [0, rows)
+hipError_t launch_gather(int bits, uint8_t *work, uint64_t S, RowSet src, int row0, int cnt, int rows, hipStream_t s);
+// One radix-4 (or radix-2) pass over rows [0, M) of work (inverse or forward).
+// groups_active: butterfly groups whose first row < mtrunc (the rest are skipped).
+hipError_t launch_pass(int bits, bool inverse, uint8_t *work, uint64_t S, int dist, int radix, int groups_active,
+                       const uint32_t *tw_pass, hipStream_t s);
+// dst[r] ^= src[r] for r in [0, rows)
+hipError_t launch_xor_rows(int bits, uint8_t *dst, const uint8_t *src, uint64_t S, int rows, hipStream_t s);
+// out.row(r) = work[r]  (verify: compare, set *mismatch)
+hipError_t launch_copy_out(int bits, RowSet out, const uint8_t *work, uint64_t S, int rows, int *mismatch,
+                           hipStream_t s);
+// work[r] = src[r] ? src[r] * tw[r] : 0 for r in [0, rows); src: device array of row pointers
+hipError_t launch_scale_in(int bits, uint8_t *work, uint64_t S, const uint8_t *const *src, const uint32_t *tw, int rows,
+                           hipStream_t s);
+// In-place formal derivative over n rows (leopard16.go:527-530, closed form).
+hipError_t launch_formal_derivative(int bits, uint8_t *work, uint64_t S, int n, hipStream_t s);
+// dst[i] = work[pos[i]] * tw[i] for i in [0, count)
+hipError_t launch_reveal(int bits, uint8_t *const *dst, const uint8_t *work, uint64_t S, const int *pos,
+                         const uint32_t *tw, int count, hipStream_t s);
+
+}  // namespace rs

@@ -1,0 +1,266 @@
+"""GPU parity tests: the HIP engine (through the C-ABI) against the oracle.
+
+Bit-exact comparison on seeded inputs at sizes the oracle finishes in
+seconds; at the BASELINE configs' full sizes, size-independent properties
+(encode -> erase -> reconstruct round trips, Verify, and column-window parity:
+shard columns are independent, so any 64-byte-aligned byte window of the GPU
+output must equal the oracle run on that window of the input).
+"""
+import numpy as np
+import pytest
+
+import reedsolomon16_amd as rs
+from oracle import orc
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_data(rng, k, S):
+    return rng.integers(0, 256, (k, S), dtype=np.uint8)
+
+
+def gpu_encode(bits, k, p, data):
+    c = rs.ReedSolomon(k, p, bits)
+    S = data.shape[1]
+    shards = [np.ascontiguousarray(data[i]) for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+    c.encode(shards)
+    return np.stack(shards[k:]), c
+
+
+# (k, p, S): every register-kernel width (m = 1..32), tails (k % m != 0), k < m,
+# the multi-pass path (m >= 64) and the reference tests' own configs
+# (reedsolomon_test.go:33-131).
+ENCODE_CASES = [
+    (2, 1, 64), (3, 1, 128), (4, 2, 256), (10, 4, 1024), (5, 3, 64), (8, 4, 192), (16, 4, 320),
+    (10, 6, 128), (20, 8, 64), (33, 17, 128), (100, 28, 64), (128, 32, 256), (130, 32, 64),
+    (3, 7, 64), (1, 1, 64), (1, 5, 64), (37, 9, 64), (128, 128, 128), (200, 100, 64),
+    (70, 40, 128), (300, 64, 64), (64, 65, 64),
+]
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+@pytest.mark.parametrize("k,p,S", ENCODE_CASES)
+def test_encode_matches_oracle(bits, k, p, S):
+    if bits == 8 and k + p > 256:
+        pytest.skip("GF(2^8) codec is for <= 256 shards")
+    rng = np.random.default_rng(k * 1000 + p * 7 + S + bits)
+    data = rand_data(rng, k, S)
+    o = orc.Oracle(bits, k, p)
+    shards = [np.ascontiguousarray(data[i]) for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+    eo = o.encode(shards)
+    c = rs.ReedSolomon(k, p, bits)
+    gs = [d.copy() for d in shards[:k]] + [np.zeros(S, np.uint8) for _ in range(p)]
+    if eo == 50:
+        with pytest.raises(rs.ErrPanic):
+            c.encode(gs)
+        return
+    assert eo == 0
+    c.encode(gs)
+    for i in range(p):
+        assert np.array_equal(gs[k + i], shards[k + i]), f"parity row {i} differs (path {c.encode_path})"
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+def test_special_inputs(bits):
+    """All-zero, all-0xFF and single-symbol impulses (BASELINE.md inputs)."""
+    k, p, S = 12, 5, 128
+    c = rs.ReedSolomon(k, p, bits)
+    cases = [np.zeros((k, S), np.uint8), np.full((k, S), 0xFF, np.uint8)]
+    for r in (0, 5, 11):
+        d = np.zeros((k, S), np.uint8)
+        d[r, 3] = 1
+        d[r, 40] = 0x80
+        cases.append(d)
+    for d in cases:
+        ref = orc.encode(bits, k, p, d)
+        shards = [d[i].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+        c.encode(shards)
+        assert np.array_equal(np.stack(shards[k:]), ref)
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+def test_verify(bits):
+    """testVerify (reedsolomon_test.go:313-411)."""
+    k, p, S = 10, 4, 1024
+    rng = np.random.default_rng(5)
+    data = rand_data(rng, k, S)
+    par, c = gpu_encode(bits, k, p, data)
+    shards = [data[i].copy() for i in range(k)] + [par[i].copy() for i in range(p)]
+    assert c.verify(shards)
+    shards[0][0] ^= 0xFF
+    assert not c.verify(shards)
+    shards[0][0] ^= 0xFF
+    shards[k + p - 1][S - 1] ^= 1
+    assert not c.verify(shards)
+
+
+RECON_CASES = [(4, 2, 128), (10, 4, 256), (16, 4, 64), (128, 32, 128), (33, 17, 64), (200, 100, 64), (5, 3, 64),
+               (2, 1, 64), (64, 65, 64)]
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+@pytest.mark.parametrize("k,p,S", RECON_CASES)
+def test_reconstruct_round_trip(bits, k, p, S):
+    if bits == 8 and k + p > 256:
+        pytest.skip("GF(2^8) codec is for <= 256 shards")
+    rng = np.random.default_rng(k + 31 * p + bits)
+    data = rand_data(rng, k, S)
+    par, c = gpu_encode(bits, k, p, data)
+    full = [data[i].copy() for i in range(k)] + [par[i].copy() for i in range(p)]
+    for trial in range(4):
+        ne = int(rng.integers(1, p + 1)) if trial else p
+        er = set(rng.choice(k + p, ne, replace=False).tolist())
+        sh = [None if i in er else full[i].copy() for i in range(k + p)]
+        c.reconstruct(sh)
+        for i in range(k + p):
+            assert np.array_equal(sh[i], full[i]), f"shard {i} (erased={i in er})"
+        # ReconstructData leaves missing parity missing
+        sh = [None if i in er else full[i].copy() for i in range(k + p)]
+        c.reconstruct_data(sh)
+        for i in range(k + p):
+            if i < k:
+                assert np.array_equal(sh[i], full[i])
+            elif i in er:
+                assert sh[i] is None
+
+
+def test_reconstruct_errors():
+    c = rs.New16(10, 4)
+    S = 64
+    sh = [np.zeros(S, np.uint8) for _ in range(14)]
+    c.encode(sh)
+    bad = [None] * 5 + sh[5:]
+    with pytest.raises(rs.ErrTooFewShards):
+        c.reconstruct(bad)
+    with pytest.raises(rs.ErrShardNoData):
+        c.reconstruct([None] * 14)
+    with pytest.raises(rs.ErrShardSize):
+        c.reconstruct([np.zeros(128, np.uint8)] + [None] + sh[2:])
+    # nothing missing: no-op
+    c.reconstruct(sh)
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    return torch
+
+
+@pytest.mark.parametrize("bits,k,p,S", [(16, 128, 32, 4096), (8, 10, 4, 4096), (16, 20, 8, 1024), (16, 300, 64, 256)])
+def test_device_encode_strided_and_table(torch_dev, bits, k, p, S):
+    torch = torch_dev
+    rng = np.random.default_rng(11)
+    data = rand_data(rng, k, S)
+    ref = orc.encode(bits, k, p, data)
+    c = rs.ReedSolomon(k, p, bits)
+    slab = torch.zeros((k + p, S), dtype=torch.uint8, device="cuda")
+    slab[:k] = torch.from_numpy(data).cuda()
+    c.encode_dev(slab)
+    torch.cuda.synchronize()
+    assert np.array_equal(slab[k:].cpu().numpy(), ref)
+    # separately allocated rows (non-strided -> device row table)
+    rows = [torch.from_numpy(data[i].copy()).cuda() for i in range(k)] + \
+           [torch.zeros(S, dtype=torch.uint8, device="cuda") for _ in range(p)]
+    c.encode_dev(rows)
+    torch.cuda.synchronize()
+    assert np.array_equal(np.stack([r.cpu().numpy() for r in rows[k:]]), ref)
+    assert c.verify_dev(rows)
+    rows[k][5] ^= 1
+    assert not c.verify_dev(rows)
+
+
+def test_device_batch(torch_dev):
+    torch = torch_dev
+    k, p, S, n = 16, 8, 2048, 5
+    rng = np.random.default_rng(3)
+    c = rs.New16(k, p)
+    slab = torch.zeros((n, k + p, S), dtype=torch.uint8, device="cuda")
+    datas = [rand_data(rng, k, S) for _ in range(n)]
+    for j in range(n):
+        slab[j, :k] = torch.from_numpy(datas[j]).cuda()
+    c.encode_dev_batch(slab)
+    torch.cuda.synchronize()
+    for j in range(n):
+        assert np.array_equal(slab[j, k:].cpu().numpy(), orc.encode(16, k, p, datas[j]))
+
+
+def test_device_reconstruct(torch_dev):
+    torch = torch_dev
+    k, p, S = 128, 32, 8192
+    rng = np.random.default_rng(9)
+    data = rand_data(rng, k, S)
+    c = rs.New16(k, p)
+    slab = torch.zeros((k + p, S), dtype=torch.uint8, device="cuda")
+    slab[:k] = torch.from_numpy(data).cuda()
+    c.encode_dev(slab)
+    torch.cuda.synchronize()
+    full = slab.clone()
+    er = rng.choice(k + p, p, replace=False)
+    present = np.ones(k + p, bool)
+    present[er] = False
+    slab[torch.from_numpy(er).cuda()] = 0
+    c.reconstruct_dev(slab, present)
+    torch.cuda.synchronize()
+    assert torch.equal(slab, full)
+
+
+# ------------------------------------------------------------------ BASELINE configs at full size
+def _window_check(bits, k, p, data_dev, par_dev, rng, width=4096, nwin=3):
+    """GPU parity on random 64-B-aligned column windows == oracle on the window."""
+    S = data_dev.shape[1]
+    for _ in range(nwin):
+        a = int(rng.integers(0, (S - width) // 64 + 1)) * 64
+        d = data_dev[:, a:a + width].cpu().numpy()
+        ref = orc.encode(bits, k, p, np.ascontiguousarray(d))
+        assert np.array_equal(par_dev[:, a:a + width].cpu().numpy(), ref), f"window @{a}"
+
+
+@pytest.mark.parametrize("bits,k,p,S", [(8, 10, 4, 1 << 20), (16, 128, 32, 1 << 20), (16, 1024, 256, 256 << 10)])
+def test_baseline_config_encode(torch_dev, bits, k, p, S):
+    """C2 / C3 / C5 encode at full size: column-window parity + verify."""
+    torch = torch_dev
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED)
+    slab = torch.randint(0, 256, (k + p, S), dtype=torch.uint8, device="cuda", generator=g)
+    c = rs.ReedSolomon(k, p, bits)
+    c.encode_dev(slab)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(1)
+    _window_check(bits, k, p, slab[:k], slab[k:], rng, width=2048 if k > 512 else 4096)
+    assert c.verify_dev(slab)
+
+
+def test_baseline_c3_full_oracle(torch_dev):
+    """C3 (128+32 x 1 MiB) bit-exact against the oracle over the whole stripe."""
+    torch = torch_dev
+    k, p, S = 128, 32, 1 << 20
+    rng = np.random.default_rng(0x5EED)
+    data = rand_data(rng, k, S)
+    ref = orc.encode(16, k, p, data)
+    slab = torch.zeros((k + p, S), dtype=torch.uint8, device="cuda")
+    slab[:k] = torch.from_numpy(data).cuda()
+    rs.New16(k, p).encode_dev(slab)
+    torch.cuda.synchronize()
+    assert np.array_equal(slab[k:].cpu().numpy(), ref)
+
+
+def test_baseline_c4_reconstruct(torch_dev):
+    """C4: 128+32 x 1 MiB, 32 random erasures (fixed seed) + worst case first 32 data shards."""
+    torch = torch_dev
+    k, p, S = 128, 32, 1 << 20
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    slab = torch.randint(0, 256, (k + p, S), dtype=torch.uint8, device="cuda", generator=g)
+    c = rs.New16(k, p)
+    c.encode_dev(slab)
+    torch.cuda.synchronize()
+    full = slab.clone()
+    rng = np.random.default_rng(0x5EED)
+    for er in (rng.choice(k + p, p, replace=False), np.arange(p)):
+        present = np.ones(k + p, bool)
+        present[er] = False
+        slab[torch.from_numpy(np.asarray(er)).cuda()] = 0
+        c.reconstruct_dev(slab, present)
+        torch.cuda.synchronize()
+        assert torch.equal(slab, full)
