@@ -88,7 +88,7 @@ def main():
     codec = rs.New16(K, P, device=dev.index)
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED + rank)
-    slab = torch.randint(0, 256, (K + P, S), dtype=torch.uint8, device=dev, generator=g)
+    slab = torch.randint(0, 256, (1, K + P, S), dtype=torch.uint8, device=dev, generator=g)
     stream = torch.cuda.current_stream()
 
     def barrier():
@@ -97,7 +97,7 @@ def main():
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        codec.encode_dev(slab, stream)
+        codec.encode_dev_batch(slab, stream)
     barrier()
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -105,7 +105,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
-        codec.encode_dev(slab, stream)
+        codec.encode_dev_batch(slab, stream)
         ev[i][1].record(stream)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0

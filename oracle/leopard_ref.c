@@ -593,13 +593,15 @@ static inline uint8_t add_mod8(uint8_t a, uint8_t b) { unsigned s = (unsigned)a 
 static inline uint8_t sub_mod8(uint8_t a, uint8_t b) { unsigned d = (unsigned)a - (unsigned)b; return (uint8_t)(d + (d >> 8)); }
 static inline uint8_t mul_log8(uint8_t a, uint8_t log_b) { return a == 0 ? 0 : expLUT8[add_mod8(logLUT8[a], log_b)]; }
 
-/* fwht8: leopard8.go:959-994 */
+/* fwht8: leopard8.go:959-994.  data is a [256]ffe8 indexed with uint16
+ * offsets, so an index >= 256 is a Go bounds-check panic. */
 static void fwht8(uint8_t *data, int mtrunc) {
     int dist = 1, dist4 = 4;
     while (dist4 <= ORDER8) {
         for (int r = 0; r < mtrunc; r += dist4) {
             uint16_t d = (uint16_t)dist, off = (uint16_t)r;
             for (uint16_t i = 0; i < d; i++) {
+                if ((unsigned)off + 3u * d >= ORDER8) GO_PANIC();
                 uint8_t t0 = data[off], t1 = data[off + d], t2 = data[off + d * 2], t3 = data[off + d * 3];
                 uint8_t a, b;
                 a = add_mod8(t0, t1); b = sub_mod8(t0, t1); t0 = a; t1 = b;

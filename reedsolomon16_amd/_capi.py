@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librs_mi355x.so")
+# RS_MI355X_LIB overrides the library path (used by scripts/ablate.sh experiment builds).
+LIB_PATH = os.environ.get("RS_MI355X_LIB") or os.path.join(_HERE, "librs_mi355x.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "rs_mi355x.h")
 
 _lib = None

@@ -115,9 +115,10 @@ struct rs_codec {
 
 namespace {
 
+// Butterfly twiddle tables (zero twiddles as all-zero tables).
 int upload_twiddles(rs_codec *c, const std::vector<uint32_t> &logs, DevBuf<uint32_t> &dst) {
     std::vector<uint32_t> host(std::max<size_t>(logs.size(), 1) * c->twd, 0);
-    for (size_t i = 0; i < logs.size(); i++) make_twiddle(*c->F, logs[i], host.data() + i * c->twd);
+    for (size_t i = 0; i < logs.size(); i++) make_twiddle(*c->F, logs[i], host.data() + i * c->twd, true);
     HIP_TRY(dst.ensure(host.size()));
     HIP_TRY(hipMemcpy(dst.p, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     return RS_OK;

@@ -121,7 +121,7 @@ const Field &field(int bits) {
 //   dword layout: [g0 lo-out: e0-3, e4-7][g0 hi-out][g1 lo][g1 hi][g2 lo][g2 hi]
 //                 [g3 lo][g3 hi][g4 lo][g4 hi][g5 lo][g5 hi][log_m][pad x3]
 //   GF(2^8) groups: (0,3) (3,3) (6,2); layout [g0: e0-3, e4-7][g1][g2][log_m][pad x2]
-void make_twiddle(const Field &F, uint32_t log_m, uint32_t *out) {
+void make_twiddle(const Field &F, uint32_t log_m, uint32_t *out, bool zero_if_mod) {
     static const int off16[6] = {0, 3, 6, 8, 11, 14}, wid16[6] = {3, 3, 2, 3, 3, 2};
     static const int off8[3] = {0, 3, 6}, wid8[3] = {3, 3, 2};
     const int ng = F.bits == 16 ? 6 : 3;
@@ -132,7 +132,8 @@ void make_twiddle(const Field &F, uint32_t log_m, uint32_t *out) {
     for (int g = 0; g < ng; g++) {
         for (int o = 0; o < nout; o++) {
             uint8_t e[8] = {0};
-            for (int x = 0; x < (1 << wid[g]); x++) e[x] = (uint8_t)(F.mul_log((uint32_t)x << off[g], log_m) >> (8 * o));
+            if (!(zero_if_mod && log_m == F.mod))
+                for (int x = 0; x < (1 << wid[g]); x++) e[x] = (uint8_t)(F.mul_log((uint32_t)x << off[g], log_m) >> (8 * o));
             out[d++] = e[0] | (e[1] << 8) | (e[2] << 16) | ((uint32_t)e[3] << 24);
             if (wid[g] == 3) out[d++] = e[4] | (e[5] << 8) | (e[6] << 16) | ((uint32_t)e[7] << 24);
         }
@@ -256,6 +257,12 @@ bool encode_schedule(const Field &F, int k, int p, std::vector<uint32_t> &ifft, 
     }
     SkewView sv{F, 0};
     fft_logs(sv, logm, p, fft.data());
+    // The fused kernels hard-code the r = 0 group's m01/m02 (and the radix-2
+    // r = 0 twiddle) as XOR-only: fftSkew[2^j - 1] == log(0).
+    for (const PassInfo &ps : fft_passes(logm)) {
+        if (ps.radix == 4 && (fft[ps.slot_off] != F.mod || fft[ps.slot_off + 1] != F.mod)) return false;
+        if (ps.radix == 2 && fft[ps.slot_off] != F.mod) return false;
+    }
     return sv.ok;
 }
 

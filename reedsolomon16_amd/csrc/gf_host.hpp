@@ -40,7 +40,11 @@ struct Field {
 const Field &field(int bits);  // built once, thread-safe
 
 // Perm-table image of "multiply by exp(log_m)" for the GPU (kTwDwords* dwords).
-void make_twiddle(const Field &F, uint32_t log_m, uint32_t *out);
+// Butterfly twiddles (zero_if_mod = true): log_m == mod is the zero twiddle of
+// the reference's XOR-only butterflies, shipped as an all-zero table.
+// mulgf16 scalings (zero_if_mod = false): log 65535 is the identity there
+// (refMul through mul16LUTs[65535], leopard16.go:810-825).
+void make_twiddle(const Field &F, uint32_t log_m, uint32_t *out, bool zero_if_mod = false);
 inline int tw_dwords(int bits) { return bits == 16 ? kTwDwords16 : kTwDwords8; }
 
 inline int ceil_pow2(int n) { return n <= 1 ? 1 : 1 << (64 - __builtin_clzll((unsigned long long)(n - 1))); }

@@ -18,8 +18,46 @@
 //   log_m == modulus means a zero twiddle: XOR only (wave-uniform branch).
 #include "kernels.hpp"
 
+// Performance-experiment knobs (scripts/ablate.sh builds separate libraries
+// with these; the product build defines none of them):
+//   RS_ABL_NO_DMA      fused encode: skip the HBM->LDS staging (computes on stale LDS)
+//   RS_ABL_ONE_TW      fused encode: every butterfly uses twiddle slot 0
+//   RS_ABL_NO_MUL      fused encode: butterflies are XOR-only
+#ifndef RS_ABL_NO_DMA
+#define RS_ABL_NO_DMA 0
+#endif
+#ifndef RS_ABL_ONE_TW
+#define RS_ABL_ONE_TW 0
+#endif
+#ifndef RS_ABL_NO_MUL
+#define RS_ABL_NO_MUL 0
+#endif
+// RS_ABL_TAB_ONCE: fused encode reads one twiddle table per transform (wrong results)
+#ifndef RS_ABL_TAB_ONCE
+#define RS_ABL_TAB_ONCE 0
+#endif
+// RS_STAMP: fused encode records per-wave (s_memtime, s_memrealtime) deltas in
+// g_rs_stamps (diagnostic builds only: scripts/micro/encode_lab.hip)
+#ifndef RS_STAMP
+#define RS_STAMP 0
+#endif
+#if RS_STAMP
+__device__ unsigned long long g_rs_stamps[1 << 16];
+#endif
+// RS_OP_FENCE: scheduling fence after every butterfly op of the fused kernels.
+#ifndef RS_OP_FENCE
+#define RS_OP_FENCE 0
+#endif
+// RS_OP_PIN: chain every butterfly op's outputs with an empty asm (bounds code motion).
+#ifndef RS_OP_PIN
+#define RS_OP_PIN 1
+#endif
+
 namespace rs {
 namespace {
+
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
 
 template <int W> struct VecOf;
 template <> struct VecOf<1> { typedef uint32_t T; };
@@ -29,7 +67,7 @@ template <> struct VecOf<4> { typedef uint32_t T __attribute__((ext_vector_type(
 template <int W>
 __device__ __forceinline__ void ldw(const uint8_t *p, uint32_t (&v)[W]) {
     typedef typename VecOf<W>::T T;
-    const T x = *reinterpret_cast<const T *>(p);
+    const T x = *(const __attribute__((address_space(1))) T *)(p);
     if constexpr (W == 1) {
         v[0] = x;
     } else {
@@ -47,11 +85,27 @@ __device__ __forceinline__ void stw(uint8_t *p, const uint32_t (&v)[W]) {
 #pragma unroll
         for (int i = 0; i < W; i++) x[i] = v[i];
     }
-    *reinterpret_cast<T *>(p) = x;
+    *(__attribute__((address_space(1))) T *)(p) = x;
+}
+// LDS (address space 3) loads of W dwords.
+template <int W>
+__device__ __forceinline__ void ldw_lds(const uint8_t *p, uint32_t (&v)[W]) {
+    typedef typename VecOf<W>::T T;
+    const T x = *(const __attribute__((address_space(3))) T *)(p);
+    if constexpr (W == 1) {
+        v[0] = x;
+    } else {
+#pragma unroll
+        for (int i = 0; i < W; i++) v[i] = x[i];
+    }
 }
 
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
     return __builtin_amdgcn_perm(s0, s1, sel);
+}
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
 // ---------------------------------------------------------------- GF(2^16)
@@ -59,6 +113,7 @@ template <int W_>
 struct F16 {
     static constexpr int W = W_;
     static constexpr int TWD = 24;     // dwords per twiddle table
+    static constexpr int TWU = 20;     // dwords used by mul_add
     static constexpr int LOGIDX = 20;  // dword holding log_m
     static constexpr uint32_t MOD = 65535;
     static constexpr int UPB = 8 / W;  // units per 64-byte block
@@ -85,6 +140,25 @@ struct F16 {
         for (int i = 0; i < W; i++) v.l[i] = v.h[i] = 0;
         return v;
     }
+    // ---- LDS staging of one wave's 64 units of a row (512*W bytes).
+    // Row image: [lo halves of blocks 0..4W) [hi halves of blocks 0..4W)
+    //            [lo halves of blocks 4W..8W) [hi halves of blocks 4W..8W)
+    // so lane l reads its lo dwords at (l/32)*256W + (l%32)*4W and its hi dwords
+    // 128W bytes later: consecutive lanes hit consecutive banks (conflict-free).
+    static constexpr int ROWB = 512 * W;
+    __device__ static uint64_t span_off(uint64_t u0) { return (u0 / UPB) * 64; }
+    // Global byte offset (within the wave span) of the 16-byte LDS piece s.
+    __device__ static uint32_t piece_goff(uint32_t s) {
+        const uint32_t G = s / (8 * W), t = s % (8 * W);
+        return ((G >> 1) * 4 * W + (t >> 1)) * 64 + (G & 1) * 32 + (t & 1) * 16;
+    }
+    __device__ static Vec lds_load(const uint8_t *img, int lane) {
+        Vec v;
+        const uint8_t *p = img + (lane >> 5) * (256 * W) + (lane & 31) * (4 * W);
+        ldw_lds<W>(p, v.l);
+        ldw_lds<W>(p + 128 * W, v.h);
+        return v;
+    }
     __device__ static void xor_into(Vec &a, const Vec &b) {
 #pragma unroll
         for (int i = 0; i < W; i++) {
@@ -98,6 +172,12 @@ struct F16 {
         for (int i = 0; i < W; i++) d |= (a.l[i] ^ b.l[i]) | (a.h[i] ^ b.h[i]);
         return d;
     }
+    // Empty asm that "redefines" the registers: chains the op that produced
+    // them ahead of this point (bounds code motion in the unrolled op lists).
+    __device__ static void pin(Vec &v) {
+#pragma unroll
+        for (int i = 0; i < W; i++) asm volatile("" : "+v"(v.l[i]), "+v"(v.h[i]));
+    }
     // x ^= y * exp(log_m); t = twiddle table (wave-uniform).
     __device__ static void mul_add(Vec &x, const Vec &y, const uint32_t *__restrict__ t) {
 #pragma unroll
@@ -105,10 +185,12 @@ struct F16 {
             const uint32_t lo = y.l[i], hi = y.h[i];
             const uint32_t a0 = lo & 0x07070707u, a1 = (lo >> 3) & 0x07070707u, a2 = (lo >> 6) & 0x03030303u;
             const uint32_t b0 = hi & 0x07070707u, b1 = (hi >> 3) & 0x07070707u, b2 = (hi >> 6) & 0x03030303u;
-            x.l[i] ^= perm(t[1], t[0], a0) ^ perm(t[5], t[4], a1) ^ perm(t[8], t[8], a2) ^ perm(t[11], t[10], b0) ^
-                      perm(t[15], t[14], b1) ^ perm(t[18], t[18], b2);
-            x.h[i] ^= perm(t[3], t[2], a0) ^ perm(t[7], t[6], a1) ^ perm(t[9], t[9], a2) ^ perm(t[13], t[12], b0) ^
-                      perm(t[17], t[16], b1) ^ perm(t[19], t[19], b2);
+            x.l[i] = xor3(xor3(xor3(x.l[i], perm(t[1], t[0], a0), perm(t[5], t[4], a1)), perm(t[8], t[8], a2),
+                               perm(t[11], t[10], b0)),
+                          perm(t[15], t[14], b1), perm(t[18], t[18], b2));
+            x.h[i] = xor3(xor3(xor3(x.h[i], perm(t[3], t[2], a0), perm(t[7], t[6], a1)), perm(t[9], t[9], a2),
+                               perm(t[13], t[12], b0)),
+                          perm(t[17], t[16], b1), perm(t[19], t[19], b2));
         }
     }
 };
@@ -118,6 +200,7 @@ template <int W_>
 struct F8 {
     static constexpr int W = W_;
     static constexpr int TWD = 8;
+    static constexpr int TWU = 5;
     static constexpr int LOGIDX = 5;
     static constexpr uint32_t MOD = 255;
     struct Vec {
@@ -137,6 +220,15 @@ struct F8 {
         for (int i = 0; i < W; i++) v.b[i] = 0;
         return v;
     }
+    // LDS staging: natural layout, lane l at l*4W (conflict-free).
+    static constexpr int ROWB = 256 * W;
+    __device__ static uint64_t span_off(uint64_t u0) { return u0 * (4 * W); }
+    __device__ static uint32_t piece_goff(uint32_t s) { return s * 16; }
+    __device__ static Vec lds_load(const uint8_t *img, int lane) {
+        Vec v;
+        ldw_lds<W>(img + lane * (4 * W), v.b);
+        return v;
+    }
     __device__ static void xor_into(Vec &a, const Vec &b) {
 #pragma unroll
         for (int i = 0; i < W; i++) a.b[i] ^= b.b[i];
@@ -147,12 +239,16 @@ struct F8 {
         for (int i = 0; i < W; i++) d |= a.b[i] ^ b.b[i];
         return d;
     }
+    __device__ static void pin(Vec &v) {
+#pragma unroll
+        for (int i = 0; i < W; i++) asm volatile("" : "+v"(v.b[i]));
+    }
     __device__ static void mul_add(Vec &x, const Vec &y, const uint32_t *__restrict__ t) {
 #pragma unroll
         for (int i = 0; i < W; i++) {
             const uint32_t v = y.b[i];
             const uint32_t a0 = v & 0x07070707u, a1 = (v >> 3) & 0x07070707u, a2 = (v >> 6) & 0x03030303u;
-            x.b[i] ^= perm(t[1], t[0], a0) ^ perm(t[3], t[2], a1) ^ perm(t[4], t[4], a2);
+            x.b[i] = xor3(x.b[i] ^ perm(t[1], t[0], a0), perm(t[3], t[2], a1), perm(t[4], t[4], a2));
         }
     }
 };
@@ -168,6 +264,25 @@ __device__ __forceinline__ void fft2(typename F::Vec &x, typename F::Vec &y, con
     if (t[F::LOGIDX] != F::MOD) F::mul_add(x, y, t);
     F::xor_into(y, x);
 }
+// Branch-free forms for the fused register kernels: a zero twiddle is shipped
+// as an all-zero table (product 0), so every multiply is straight-line code
+// and the scalar table loads can be hoisted.  XOR-only (X) forms are used
+// where the twiddle is zero by construction.
+template <class F>
+__device__ __forceinline__ void ifft2m(typename F::Vec &x, typename F::Vec &y, const uint32_t *__restrict__ t) {
+    F::xor_into(y, x);
+    F::mul_add(x, y, t);
+}
+template <class F>
+__device__ __forceinline__ void fft2m(typename F::Vec &x, typename F::Vec &y, const uint32_t *__restrict__ t) {
+    F::mul_add(x, y, t);
+    F::xor_into(y, x);
+}
+template <class F>
+__device__ __forceinline__ void fft2x(typename F::Vec &x, typename F::Vec &y) {
+    F::xor_into(y, x);
+}
+
 // Slot order of a radix-4 group: t[0] = m01, t[1] = m02, t[2] = m23 (each F::TWD dwords).
 template <class F>
 __device__ __forceinline__ void ifft4(typename F::Vec &x0, typename F::Vec &x1, typename F::Vec &x2,
@@ -199,92 +314,301 @@ __device__ __forceinline__ uint8_t *row_ptr(const RowSet &rs, int i) {
 }
 
 // ---------------------------------------------------------------- register transforms (M <= 32)
-// ifftDITEncoder transform (leopard16.go:694-741): radix-4 pairs at dist 1,4,16,
-// then a radix-2 layer at M/2 when log2(M) is odd.  Groups with r >= mtrunc
-// hold only zero rows and are skipped (uniform branch), as in the reference.
-template <class F, int LOGM>
-__device__ __forceinline__ void ifft_reg(typename F::Vec (&w)[1 << LOGM], const uint32_t *__restrict__ tw, int mtrunc) {
-    constexpr int M = 1 << LOGM;
-    int slot = 0;
-#pragma unroll
-    for (int dist = 1; dist * 4 <= M; dist *= 4) {
-#pragma unroll
-        for (int r = 0; r < M; r += 4 * dist) {
-            const uint32_t *t = tw + slot * F::TWD;
-            slot += 3;
-            if (r < mtrunc) {
-#pragma unroll
-                for (int i = r; i < r + dist; i++) ifft4<F>(w[i], w[i + dist], w[i + 2 * dist], w[i + 3 * dist], t);
+// A transform is a compile-time list of radix-2 butterfly ops over the M
+// registers.  Kinds: IFFT (y ^= x; x ^= y*t), FFT (x ^= y*t; y ^= x) and
+// FFT-XOR (y ^= x, zero twiddle).  Orders and twiddle slots follow
+//   ifftDITEncoder leopard16.go:694-741: radix-4 pairs at dist 1,4,16 (m01 on
+//     (i,i+d), m23 on (i+2d,i+3d), then m02 on (i,i+2d),(i+d,i+3d)), and a
+//     radix-2 layer at M/2 when log2(M) is odd;
+//   fftDIT leopard16.go:618-657: radix-4 pairs at dist M/4, M/16, ... (m02
+//     first, then m01 / m23), and a radix-2 layer at dist 1 when log2(M) is odd.
+// The reference skips IFFT groups with r >= mtrunc: those rows are zero here,
+// and any twiddle maps zero rows to zero rows, so computing them is equivalent.
+// In the FFT, the r = 0 group's m01 = fftSkew[dist-1] and m02 = fftSkew[2*dist-1]
+// (and the radix-2 fftSkew[0]) are fftSkew[2^j - 1] = log(0) (initFFTSkew
+// leopard16.go:997), so they are XOR-only by construction (checked on the host
+// in encode_schedule).  FFT rows >= p are computed but never stored.
+enum : int { OP_IFFT = 0, OP_FFT = 1, OP_FFTX = 2 };
+struct BOp {
+    int x, y, slot, kind;
+};
+// Within a radix-4 group the ops are ordered by twiddle (all m01 butterflies,
+// then all m23, then all m02 for the IFFT; m02, m01, m23 for the FFT) so
+// consecutive ops share a table; this is legal because butterflies of one
+// layer over different i are independent.
+template <int LOGM>
+struct IfftOps {
+    static constexpr int M = 1 << LOGM, N = (M / 2) * LOGM;
+    BOp op[N > 0 ? N : 1];
+    constexpr IfftOps() : op() {
+        int n = 0, slot = 0, dist = 1;
+        for (; dist * 4 <= M; dist *= 4)
+            for (int r = 0; r < M; r += 4 * dist, slot += 3) {
+                for (int i = r; i < r + dist; i++) op[n++] = BOp{i, i + dist, slot, OP_IFFT};                   // m01
+                for (int i = r; i < r + dist; i++) op[n++] = BOp{i + 2 * dist, i + 3 * dist, slot + 2, OP_IFFT};  // m23
+                for (int i = r; i < r + dist; i++) {                                                             // m02
+                    op[n++] = BOp{i, i + 2 * dist, slot + 1, OP_IFFT};
+                    op[n++] = BOp{i + dist, i + 3 * dist, slot + 1, OP_IFFT};
+                }
             }
+        if (dist < M)
+            for (int i = 0; i < M / 2; i++) op[n++] = BOp{i, i + M / 2, slot, OP_IFFT};
+    }
+};
+template <int LOGM>
+struct FftOps {
+    static constexpr int M = 1 << LOGM, N = (M / 2) * LOGM;
+    BOp op[N > 0 ? N : 1];
+    constexpr FftOps() : op() {
+        int n = 0, slot = 0, dist = M / 4;
+        for (; dist != 0; dist /= 4)
+            for (int r = 0; r < M; r += 4 * dist, slot += 3) {
+                const int k0 = r == 0 ? OP_FFTX : OP_FFT;
+                for (int i = r; i < r + dist; i++) {  // m02
+                    op[n++] = BOp{i, i + 2 * dist, slot + 1, k0};
+                    op[n++] = BOp{i + dist, i + 3 * dist, slot + 1, k0};
+                }
+                for (int i = r; i < r + dist; i++) op[n++] = BOp{i, i + dist, slot, k0};                          // m01
+                for (int i = r; i < r + dist; i++) op[n++] = BOp{i + 2 * dist, i + 3 * dist, slot + 2, OP_FFT};  // m23
+            }
+        if (LOGM & 1)
+            for (int r = 0; r < M; r += 2) op[n++] = BOp{r, r + 1, slot + r / 2, r == 0 ? OP_FFTX : OP_FFT};
+    }
+};
+
+// Twiddle table held in registers (wave-uniform -> SGPRs).
+template <class F>
+struct Tab {
+    uint32_t v[F::TWU];
+};
+// LDS-resident table (uniform address: every lane reads the same 16-byte
+// slots, a broadcast); lands in VGPRs so both v_perm table operands are
+// VGPRs and no SGPR->VGPR copies are needed.
+template <class F>
+__device__ __forceinline__ Tab<F> lds_tab(uint32_t vaddr, int byte_off) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    Tab<F> r;
+#pragma unroll
+    for (int q = 0; q < (F::TWU + 3) / 4; q++) {
+        // volatile: keeps IR passes from hoisting all table reads of the unrolled
+        // op list together (sched_barrier only constrains the machine scheduler).
+        // vaddr lives in a VGPR, so byte_off folds into the ds_read offset field.
+        const u32x4 x = *(const volatile __attribute__((address_space(3))) u32x4 *)(uintptr_t)(vaddr + byte_off + 16 * q);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (4 * q + j < F::TWU) r.v[4 * q + j] = x[j];
+    }
+    return r;
+}
+
+// Loaded through the constant address space: read-only for the whole launch,
+// so the wave-uniform address turns into s_load_dwordx* (scalar cache).
+typedef __attribute__((address_space(4))) const uint32_t cu32_t;
+template <class F>
+__device__ __forceinline__ Tab<F> load_tab(const uint32_t *__restrict__ t) {
+    Tab<F> r;
+    cu32_t *ct = (cu32_t *)t;
+#pragma unroll
+    for (int j = 0; j < F::TWU; j++) r.v[j] = ct[j];
+    return r;
+}
+
+// Multiplying ops of a list, in order, each with the slot it reads; XOR-only
+// ops need no table.  A table is loaded once per run of equal slots.
+template <class OPS>
+struct TabRuns {
+    static constexpr int N = OPS::N;
+    int slot[N > 0 ? N : 1];  // slot of the k-th table load
+    int load_at[N > 0 ? N : 1];  // op index whose table is load k (or -1)
+    int first_use[N > 0 ? N : 1];  // table index used by op i (-1: XOR-only)
+    int count;
+    constexpr TabRuns() : slot(), load_at(), first_use(), count(0) {
+        constexpr OPS ops{};
+        int last = -1;
+        for (int i = 0; i < N; i++) {
+            if (ops.op[i].kind == OP_FFTX) { first_use[i] = -1; continue; }
+            if (ops.op[i].slot != last) {
+                slot[count] = ops.op[i].slot;
+                count++;
+                last = ops.op[i].slot;
+            }
+            first_use[i] = count - 1;
         }
     }
-    if constexpr (LOGM & 1) {
-        constexpr int d = M / 2;
-        const uint32_t *t = tw + slot * F::TWD;
+};
+
+// Runs the op list.  Twiddle tables are wave-uniform scalar loads issued two
+// tables ahead of use; scheduling fences keep each load at the top of its
+// region (the machine scheduler would otherwise sink it next to its wait)
+// and bound the VGPR pressure of the fully unrolled code.
+template <class F, class OPS>
+__device__ __forceinline__ void run_ops(typename F::Vec *w, uint32_t ltab) {
+    constexpr OPS ops{};
+    constexpr TabRuns<OPS> runs{};
+    constexpr int N = OPS::N;
+    constexpr int NT = runs.count;
+    constexpr int TB = F::TWD * 4;  // bytes per table slot
+    Tab<F> t0, t1;
+    if constexpr (NT > 0) t0 = lds_tab<F>(ltab, (RS_ABL_ONE_TW ? 0 : runs.slot[0]) * TB);
+    int have = 0;  // index of the table in t0
 #pragma unroll
-        for (int i = 0; i < d; i++) ifft2<F>(w[i], w[i + d], t);
+    for (int i = 0; i < N; i++) {
+        const BOp o = ops.op[i];
+        const int need = runs.first_use[i];
+        if (!RS_ABL_TAB_ONCE && need >= 0 && need != have) {  // next run: its table was prefetched into t1
+            t0 = t1;
+            have = need;
+        }
+        if (!RS_ABL_TAB_ONCE && need >= 0 && (i == 0 || runs.first_use[i - 1] != need)) {
+            if (have + 1 < NT) t1 = lds_tab<F>(ltab, (RS_ABL_ONE_TW ? 0 : runs.slot[have + 1 < NT ? have + 1 : 0]) * TB);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (RS_ABL_NO_MUL) {
+            F::xor_into(w[o.y], w[o.x]);
+        } else if (o.kind == OP_IFFT) {
+            F::xor_into(w[o.y], w[o.x]);
+            F::mul_add(w[o.x], w[o.y], t0.v);
+        } else if (o.kind == OP_FFT) {
+            F::mul_add(w[o.x], w[o.y], t0.v);
+            F::xor_into(w[o.y], w[o.x]);
+        } else {
+            F::xor_into(w[o.y], w[o.x]);
+        }
+#if RS_OP_PIN
+        F::pin(w[o.x]);
+        F::pin(w[o.y]);
+#endif
+#if RS_OP_FENCE
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 }
 
-// fftDIT (leopard16.go:618-657): radix-4 pairs at dist M/4, M/16, ..., then a
-// radix-2 layer at dist 1 when log2(M) is odd; groups with r >= mtrunc skipped.
 template <class F, int LOGM>
-__device__ __forceinline__ void fft_reg(typename F::Vec (&w)[1 << LOGM], const uint32_t *__restrict__ tw, int mtrunc) {
-    constexpr int M = 1 << LOGM;
-    int slot = 0;
-#pragma unroll
-    for (int dist = M / 4; dist != 0; dist /= 4) {
-#pragma unroll
-        for (int r = 0; r < M; r += 4 * dist) {
-            const uint32_t *t = tw + slot * F::TWD;
-            slot += 3;
-            if (r < mtrunc) {
-#pragma unroll
-                for (int i = r; i < r + dist; i++) fft4<F>(w[i], w[i + dist], w[i + 2 * dist], w[i + 3 * dist], t);
-            }
-        }
-    }
-    if constexpr (LOGM & 1) {
-#pragma unroll
-        for (int r = 0; r < M; r += 2) {
-            const uint32_t *t = tw + (slot + r / 2) * F::TWD;
-            if (r < mtrunc) fft2<F>(w[r], w[r + 1], t);
-        }
-    }
+__device__ __forceinline__ void ifft_reg(typename F::Vec (&w)[1 << LOGM], uint32_t ltab) {
+    if constexpr (LOGM > 0) run_ops<F, IfftOps<LOGM>>(w, ltab);
+}
+template <class F, int LOGM>
+__device__ __forceinline__ void fft_reg(typename F::Vec (&w)[1 << LOGM], uint32_t ltab) {
+    if constexpr (LOGM > 0) run_ops<F, FftOps<LOGM>>(w, ltab);
+}
+constexpr int fft_slot_count(int logm) {
+    int M = 1 << logm, s = 0, dist4 = M, dist = M >> 2;
+    for (; dist != 0; dist4 = dist, dist >>= 2) s += 3 * (M / dist4);
+    if (dist4 == 2) s += M / 2;
+    return s;
 }
 
-template <class F, int M>
-__device__ __forceinline__ void load_chunk(typename F::Vec (&w)[M], const EncodeArgs &a, int c, uint64_t soff,
-                                           uint64_t u) {
-    const int row0 = c * M;
-    const int cnt = a.k - row0;
-#pragma unroll
-    for (int r = 0; r < M; r++) {
-        if (r < cnt) w[r] = F::load(row_ptr(a.data, row0 + r) + soff, u);
-        else w[r] = F::zero();
-    }
+// 32-bit LDS address of p, materialized in a VGPR (opaque to the compiler) so
+// that constant offsets from it use the DS instruction's offset field instead
+// of one SGPR add + v_mov per access.
+__device__ __forceinline__ uint32_t vgpr_lds_addr(const uint8_t *p) {
+    const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)p;
+    uint32_t v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(a));
+    return v;
+}
+
+template <bool TABLE>
+__device__ __forceinline__ uint8_t *rowp(const RowSet &rs, int i, uint64_t soff) {
+    if constexpr (TABLE) return rs.table[i];
+    else return rs.base + (uint64_t)i * rs.stride + soff;
 }
 
 // Fused encode (leopard16.go:128-224 / leopard8.go:153-277) for m = 2^LOGM <= 32.
-// Every lane owns one column unit of all k+p rows; the m-row work set, the
-// m-row accumulator and the prefetched next chunk live in VGPRs, so HBM sees
-// exactly k reads and p writes (or p reads for verify) per unit.
-template <class F, int LOGM, bool VERIFY>
+// Every lane owns one column unit of all k+p rows; the m-row accumulator and
+// the current chunk live in VGPRs.  While chunk c is transformed, chunk c+1's
+// rows stream HBM -> LDS (global_load_lds_dwordx4, 16 B/lane, no VGPRs) into
+// the wave's private image, and its twiddle tables into the block's other
+// table buffer.  HBM sees exactly k row reads and p row writes (p reads for
+// verify) per unit.
+template <class F, int LOGM, bool VERIFY, bool TABLE>
 __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
     constexpr int M = 1 << LOGM;
+    constexpr int ROWB = F::ROWB;          // bytes of a row covered by one wave
+    constexpr int PPR = ROWB / 16;         // 16-byte pieces per row
+    constexpr int NDMA = M * PPR / 64;     // DMA wave-instructions per chunk
+    static_assert(NDMA * 64 == M * PPR, "chunk must be whole DMA instructions");
+    constexpr int IS = ifft_slot_count(LOGM), FS = fft_slot_count(LOGM);
+    constexpr int TB = F::TWD * 4;                      // bytes per twiddle table
+    constexpr int TABB = ((IS > FS ? IS : FS) * TB + 15) / 16 * 16;  // bytes per table buffer
     typedef typename F::Vec V;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint8_t lds[4 * M * ROWB + 2 * TABB];
+    uint8_t *ltab = lds + 4 * M * ROWB;
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
     const uint64_t units = F::units(a.shard_size);
-    const uint64_t u = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (u >= units) return;
+    const uint64_t u0 = (uint64_t)blockIdx.x * 256 + wave * 64;
+    const bool wave_live = u0 < units;  // waves past the row end still join the barriers
+    const uint64_t u = u0 + lane;
     const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
-    V acc[M], cur[M];
-    load_chunk<F, M>(cur, a, 0, soff, u);
+    const uint64_t span = F::span_off(u0);
+    uint8_t *img = lds + wave * (M * ROWB);
+
+    // Stage chunk c's rows: rows past the chunk's count and pieces past the
+    // row end are zero-filled.
+    auto stage = [&](int c) {
+        const int row0 = c * M, cnt = a.k - row0;
+#pragma unroll
+        for (int j = 0; j < NDMA; j++) {
+            const int P = j * 64 + lane;
+            const int r = P / PPR;
+            const uint64_t go = span + F::piece_goff(P % PPR);
+            if (RS_ABL_NO_DMA) {
+            } else if (wave_live && r < cnt && go < a.shard_size) {
+                const uint8_t *src = rowp<TABLE>(a.data, row0 + r, soff) + go;
+                __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(img + j * 1024), 16, 0, 0);
+            } else {
+                *(__attribute__((address_space(3))) u32x4 *)(img + j * 1024 + lane * 16) = u32x4{0, 0, 0, 0};
+            }
+        }
+    };
+    // Stage `nslot` twiddle tables into table buffer b (waves split the pieces).
+    auto stage_tab = [&](const uint32_t *src, int nslot, int b) {
+        const int npieces = nslot * TB / 16;
+        const int P = wave * 64 + lane;
+        for (int base = 0; base < npieces; base += 256) {
+            if (base + P < npieces)
+                __builtin_amdgcn_global_load_lds((gvoid_t *)((const uint8_t *)src + (base + P) * 16),
+                                                 (lvoid_t *)(ltab + b * TABB + base * 16 + wave * 1024), 16, 0, 0);
+        }
+    };
+
+#if RS_STAMP
+    const unsigned long long st_c0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    V acc[M];
+    stage(0);
+    stage_tab(a.tw_ifft, IS, 0);
+#if RS_STAMP
+    unsigned long long st_wait = 0, st_first = 0;
+#endif
     for (int c = 0; c < a.nchunks; ++c) {
-        V nxt[M];
-        const bool more = c + 1 < a.nchunks;
-        if (more) load_chunk<F, M>(nxt, a, c + 1, soff, u);
-        const int cnt = a.k - c * M;
-        ifft_reg<F, LOGM>(cur, a.tw_ifft + (uint64_t)c * ifft_slot_count(LOGM) * F::TWD, cnt);
+#if RS_STAMP
+        const unsigned long long sw0 = __builtin_amdgcn_s_memtime();
+#endif
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs for chunk c have landed
+        __syncthreads();  // every wave's table pieces landed; buffer (c+1)&1 is no longer read
+#if RS_STAMP
+        {
+            const unsigned long long sw1 = __builtin_amdgcn_s_memtime();
+            if (c == 0) st_first = sw1 - st_c0;
+            else st_wait += sw1 - sw0;
+        }
+#endif
+        V cur[M];
+#pragma unroll
+        for (int r = 0; r < M; r++) cur[r] = F::lds_load(img + r * ROWB, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is overwritten
+        if (c + 1 < a.nchunks) {
+            stage(c + 1);
+            stage_tab(a.tw_ifft + (uint64_t)(c + 1) * IS * F::TWD, IS, (c + 1) & 1);
+        } else {
+            stage_tab(a.tw_fft, FS, (c + 1) & 1);
+        }
+        ifft_reg<F, LOGM>(cur, vgpr_lds_addr(ltab + (c & 1) * TABB));
         if (c == 0) {
 #pragma unroll
             for (int r = 0; r < M; r++) acc[r] = cur[r];
@@ -292,22 +616,53 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
 #pragma unroll
             for (int r = 0; r < M; r++) F::xor_into(acc[r], cur[r]);
         }
-        if (more) {
-#pragma unroll
-            for (int r = 0; r < M; r++) cur[r] = nxt[r];
+    }
+#if RS_STAMP
+    const unsigned long long sf0 = __builtin_amdgcn_s_memtime();
+#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#if RS_STAMP
+    const unsigned long long sf1 = __builtin_amdgcn_s_memtime();
+#endif
+    fft_reg<F, LOGM>(acc, vgpr_lds_addr(ltab + (a.nchunks & 1) * TABB));
+#if RS_STAMP
+    const unsigned long long sf2 = __builtin_amdgcn_s_memtime();
+    if (lane == 0 && blockIdx.y == 0) {
+        const unsigned i2 = (blockIdx.x * 4 + wave) * 4 + 32768;
+        if (i2 + 3 < (1u << 16)) {
+            g_rs_stamps[i2] = st_first;
+            g_rs_stamps[i2 + 1] = st_wait + (sf1 - sf0);
+            g_rs_stamps[i2 + 2] = sf2 - sf1;
+            g_rs_stamps[i2 + 3] = sf0 - st_c0;
         }
     }
-    fft_reg<F, LOGM>(acc, a.tw_fft, a.p);
+    if (lane == 0 && blockIdx.y == 0) {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned idx = (blockIdx.x * 4 + wave) * 4;
+        if (idx + 3 < (1u << 16)) {
+            g_rs_stamps[idx] = c1 - st_c0;
+            g_rs_stamps[idx + 1] = r1 - st_r0;
+            g_rs_stamps[idx + 2] = st_r0;
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            unsigned hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            g_rs_stamps[idx + 3] = ((unsigned long long)xcc << 32) | hw;
+        }
+    }
+#endif
+    if (!wave_live || u >= units) return;
     if constexpr (VERIFY) {
         uint32_t bad = 0;
 #pragma unroll
         for (int r = 0; r < M; r++)
-            if (r < a.p) bad |= F::diff(acc[r], F::load(row_ptr(a.parity, r) + soff, u));
+            if (r < a.p) bad |= F::diff(acc[r], F::load(rowp<TABLE>(a.parity, r, soff), u));
         if (bad) atomicOr(a.mismatch, 1);
     } else {
 #pragma unroll
         for (int r = 0; r < M; r++)
-            if (r < a.p) F::store(row_ptr(a.parity, r) + soff, u, acc[r]);
+            if (r < a.p) F::store(rowp<TABLE>(a.parity, r, soff), u, acc[r]);
     }
 }
 
@@ -457,8 +812,14 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
     if constexpr (F::TWD == 24) nunits = (a.shard_size >> 6) * (8 / F::W);
     else nunits = a.shard_size / (4 * F::W);
     dim3 grid((unsigned)((nunits + 255) / 256), (unsigned)a.nstripes);
-    if (verify) hipLaunchKernelGGL((k_encode_reg<F, LOGM, true>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_encode_reg<F, LOGM, false>), grid, dim3(256), 0, s, a);
+    const bool table = a.data.table != nullptr || a.parity.table != nullptr;
+    if (table) {
+        if (verify) hipLaunchKernelGGL((k_encode_reg<F, LOGM, true, true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_encode_reg<F, LOGM, false, true>), grid, dim3(256), 0, s, a);
+    } else {
+        if (verify) hipLaunchKernelGGL((k_encode_reg<F, LOGM, true, false>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_encode_reg<F, LOGM, false, false>), grid, dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }
 

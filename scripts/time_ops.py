@@ -1,0 +1,63 @@
+"""Time device-resident codec operations with HIP events (kernel-side time,
+launches back to back).  Prints one line per config."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+CONFIGS = {
+    "C2": (8, 10, 4, 1 << 20, "encode"),
+    "C3": (16, 128, 32, 1 << 20, "encode"),
+    "C3v": (16, 128, 32, 1 << 20, "verify"),
+    "C4": (16, 128, 32, 1 << 20, "reconstruct"),
+    "C5": (16, 1024, 256, 256 << 10, "encode"),
+    "C5x8": (16, 1024, 256, 32 << 10, "encode"),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C3")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--tag", default="")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import reedsolomon16_amd as rs
+
+    for name in a.configs.split(","):
+        bits, k, p, S, op = CONFIGS[name]
+        c = rs.ReedSolomon(k, p, bits)
+        slab = torch.randint(0, 256, (1, k + p, S), dtype=torch.uint8, device="cuda")
+        rows = slab[0]
+        present = np.ones(k + p, bool)
+        present[np.random.default_rng(0x5EED).choice(k + p, p, replace=False)] = False
+
+        def run():
+            if op == "encode":
+                c.encode_dev_batch(slab)
+            elif op == "verify":
+                c.verify_dev(rows)
+            else:
+                c.reconstruct_dev(rows, present)
+
+        for _ in range(5):
+            run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / a.iters
+        alg = (k + p) * S
+        print(json.dumps({"tag": a.tag, "config": name, "op": op, "path": c.encode_path, "us": round(us, 2),
+                          "GBps_alg": round(alg / us / 1e3, 1), "frac": round(alg / us / 1e3 / 8000, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

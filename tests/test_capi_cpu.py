@@ -1,0 +1,190 @@
+"""CPU tests of the product library's C-ABI (no device calls): it loads,
+exports every function include/rs_mi355x.h declares, builds the same field
+tables as the oracle, its byte-permute twiddle images multiply correctly
+(emulating v_perm_b32 in numpy), its error locators match, and argument
+validation mirrors the reference's error behaviour."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import reedsolomon16_amd as rs
+from oracle import leopard_np as lnp
+from oracle import orc
+from reedsolomon16_amd import _capi
+
+
+def test_library_exports_header():
+    L = rs.lib()
+    names = _capi.header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_error_codes_match_oracle_numbering():
+    text = open(_capi.HEADER_PATH).read()
+    want = {"RS_ERR_INV_SHARD_NUM": 1, "RS_ERR_MAX_SHARD_NUM": 2, "RS_ERR_TOO_FEW_SHARDS": 3,
+            "RS_ERR_SHARD_NO_DATA": 4, "RS_ERR_SHARD_SIZE": 5, "RS_ERR_INVALID_SHARD_SIZE": 6,
+            "RS_ERR_NOT_SUPPORTED": 7, "RS_ERR_PANIC": 50}
+    for k, v in want.items():
+        assert f"#define {k}" in text and str(v) in text.split(f"#define {k}")[1].split("\n")[0]
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+def test_engine_tables_match_oracle(bits):
+    n = 1 << bits
+    bufs = [np.zeros(n, np.uint16), np.zeros(n, np.uint16), np.zeros(n - 1, np.uint16), np.zeros(n, np.uint16)]
+    assert rs.lib().rs_debug_field_tables(bits, *[b.ctypes.data for b in bufs]) == 0
+    ref = orc.tables16() if bits == 16 else orc.tables8()
+    for a, b in zip(bufs, ref):
+        assert np.array_equal(a.astype(np.int64), b.astype(np.int64))
+
+
+def vperm(s0, s1, sel):
+    """numpy model of v_perm_b32 (selector bytes 0..7 pick from {s0:s1}, s1 low)."""
+    data = (np.uint64(s0) << np.uint64(32)) | np.uint64(s1)
+    out = np.zeros_like(sel, dtype=np.uint32)
+    for b in range(4):
+        idx = (sel >> np.uint32(8 * b)) & np.uint32(0xFF)
+        assert np.all(idx < 8)
+        byte = (data >> (idx.astype(np.uint64) * np.uint64(8))) & np.uint64(0xFF)
+        out |= byte.astype(np.uint32) << np.uint32(8 * b)
+    return out
+
+
+def twiddle(bits, log_m):
+    L = rs.lib()
+    n = L.rs_debug_twiddle_dwords(bits)
+    t = np.zeros(n, np.uint32)
+    assert L.rs_debug_twiddle(bits, log_m, t.ctypes.data) == 0
+    return [np.uint32(x) for x in t]
+
+
+def emulate_mul16(lo, hi, t):
+    """The kernel's F16::mul_add on (lo, hi) dwords with x = 0."""
+    m7, m3 = np.uint32(0x07070707), np.uint32(0x03030303)
+    a0, a1, a2 = lo & m7, (lo >> np.uint32(3)) & m7, (lo >> np.uint32(6)) & m3
+    b0, b1, b2 = hi & m7, (hi >> np.uint32(3)) & m7, (hi >> np.uint32(6)) & m3
+    pl = vperm(t[1], t[0], a0) ^ vperm(t[5], t[4], a1) ^ vperm(t[8], t[8], a2) ^ vperm(t[11], t[10], b0) ^ \
+        vperm(t[15], t[14], b1) ^ vperm(t[18], t[18], b2)
+    ph = vperm(t[3], t[2], a0) ^ vperm(t[7], t[6], a1) ^ vperm(t[9], t[9], a2) ^ vperm(t[13], t[12], b0) ^ \
+        vperm(t[17], t[16], b1) ^ vperm(t[19], t[19], b2)
+    return pl, ph
+
+
+def test_twiddle_image_multiplies_gf16():
+    rng = np.random.default_rng(3)
+    F = lnp.field(16)
+    rows = rng.integers(0, 256, (1, 64 * 8), dtype=np.uint8)
+    sym = lnp.to_symbols(rows, 16)[0]
+    blk = rows.reshape(-1, 64)
+    lo = blk[:, :32].copy().view(np.uint32).ravel()
+    hi = blk[:, 32:].copy().view(np.uint32).ravel()
+    for log_m in list(rng.integers(0, 65535, 30)) + [0, 1, 65534, 65535]:
+        pl, ph = emulate_mul16(lo, hi, twiddle(16, int(log_m)))
+        got_blk = np.concatenate([pl.reshape(-1, 8).view(np.uint8), ph.reshape(-1, 8).view(np.uint8)], axis=1)
+        want = lnp.from_symbols(F.mul_log(sym, int(log_m))[None], 16)[0]
+        assert np.array_equal(got_blk.ravel(), want), log_m
+
+
+def test_twiddle_image_multiplies_gf8():
+    rng = np.random.default_rng(4)
+    F = lnp.field(8)
+    data = rng.integers(0, 256, 256, dtype=np.uint8)
+    d = data.view(np.uint32)
+    m7, m3 = np.uint32(0x07070707), np.uint32(0x03030303)
+    for log_m in range(256):
+        t = twiddle(8, log_m)
+        p = vperm(t[1], t[0], d & m7) ^ vperm(t[3], t[2], (d >> np.uint32(3)) & m7) ^ \
+            vperm(t[4], t[4], (d >> np.uint32(6)) & m3)
+        assert np.array_equal(p.view(np.uint8), F.mul_log(data.astype(np.int64), log_m).astype(np.uint8))
+
+
+@pytest.mark.parametrize("bits,k,p", [(16, 10, 4), (16, 128, 32), (16, 1000, 300), (8, 10, 4), (8, 100, 28)])
+def test_error_locators_match_numpy(bits, k, p):
+    rng = np.random.default_rng(k)
+    for _ in range(3):
+        erased = np.zeros(k + p, np.uint8)
+        erased[rng.choice(k + p, p, replace=False)] = 1
+        out = np.zeros(1 << bits, np.uint32)
+        assert rs.lib().rs_debug_error_locators(bits, k, p, erased.ctypes.data, out.ctypes.data) == 0
+        assert np.array_equal(out.astype(np.int64), lnp.error_locators(bits, k, p, erased.astype(bool)))
+
+
+def test_error_locators_panic_where_reference_panics():
+    erased = np.zeros(240, np.uint8)
+    out = np.zeros(256, np.uint32)
+    assert rs.lib().rs_debug_error_locators(8, 200, 40, erased.ctypes.data, out.ctypes.data) == 50
+
+
+def test_constructor_errors():
+    with pytest.raises(rs.ErrInvShardNum):
+        rs.New16(0, 4)
+    with pytest.raises(rs.ErrInvShardNum):
+        rs.New8(4, 0)
+    with pytest.raises(rs.ErrMaxShardNum):
+        rs.New16(60000, 6000)
+    c = rs.New(10, 4)
+    assert c.field_bits == 8 and c.total_shards() == 14 and c.shard_size_multiple() == 64
+    assert rs.New(200, 100).field_bits == 16
+    assert rs.New16(128, 32).encode_path == "reg16-m32"
+    assert rs.New16(1024, 256).encode_path == "multipass"
+
+
+def test_host_validation_errors_without_device():
+    """Validation happens before any device work (Encode leopard16.go:116-135,
+    reconstruct :390-430)."""
+    c = rs.New16(10, 4)
+    S = 128
+    good = [np.zeros(S, np.uint8) for _ in range(14)]
+    with pytest.raises(rs.ErrTooFewShards):
+        c.encode(good[:13])
+    with pytest.raises(rs.ErrShardSize):
+        c.encode(good[:13] + [np.zeros(64, np.uint8)])
+    with pytest.raises(rs.ErrShardSize):
+        c.encode(good[:13] + [None])
+    with pytest.raises(rs.ErrInvalidShardSize):
+        c.encode([np.zeros(100, np.uint8) for _ in range(14)])
+    with pytest.raises(rs.ErrShardNoData):
+        c.encode([None] * 14)
+    with pytest.raises(rs.ErrTooFewShards):
+        c.reconstruct([None] * 5 + good[5:])
+    with pytest.raises(rs.ErrShardNoData):
+        c.reconstruct([None] * 14)
+    with pytest.raises(rs.ErrShardSize):
+        c.reconstruct([np.zeros(64, np.uint8)] + good[1:])
+    # nothing missing: no-op, no device needed
+    assert c.reconstruct([g.copy() for g in good]) is not None
+    with pytest.raises(rs.ErrNotSupported):
+        c.encode_idx(good[0], 0, good[10:])
+    with pytest.raises(rs.ErrNotSupported):
+        c.update(good, good[:10])
+
+
+def test_encode_panic_geometry_without_device():
+    c = rs.New8(129, 127)
+    assert c.encode_path == "panic"
+    with pytest.raises(rs.ErrPanic):
+        c.encode([np.zeros(64, np.uint8) for _ in range(256)])
+
+
+def test_split_join_mirror_reference():
+    """Split/Join (leopard16.go:232-340) as used by testEncodeDecode."""
+    import io
+
+    c = rs.New16(4, 2)
+    data = (np.arange(1000) % 251).astype(np.uint8)
+    shards = c.split(data)
+    assert len(shards) == 6 and all(len(s) == 256 for s in shards)
+    buf = io.BytesIO()
+    c.join(buf, shards, len(data))
+    assert buf.getvalue() == bytes(data)
+    with pytest.raises(rs.ErrShortData):
+        c.split(b"")
+    with pytest.raises(rs.ErrReconstructRequired):
+        c.join(io.BytesIO(), [None] + shards[1:], 10)
+    with pytest.raises(rs.ErrShortData):
+        c.join(io.BytesIO(), shards, 4 * 256 + 1)
+    with pytest.raises(rs.ErrTooFewShards):
+        c.join(io.BytesIO(), shards[:3], 10)

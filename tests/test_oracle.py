@@ -1,0 +1,180 @@
+"""CPU tests of the oracle (test infrastructure): the C restatement against the
+independent numpy restatement, the golden fixtures, the survey's table
+anchors, the reference tests' round-trip properties and the reference's
+panic / error behaviour."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from oracle import leopard_np as lnp
+from oracle import orc
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_table_anchors():
+    """SURVEY.md §8c sanity anchors (fftSkew[0:8] for both fields)."""
+    _, _, skew16, _ = orc.tables16()
+    _, _, skew8, _ = orc.tables8()
+    assert skew16[:8].tolist() == [65535, 65535, 21845, 65535, 17476, 21845, 34952, 65535]
+    assert skew8[:8].tolist() == [255, 255, 85, 255, 17, 85, 34, 255]
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+def test_tables_c_vs_numpy(bits):
+    t = orc.tables16() if bits == 16 else orc.tables8()
+    F = lnp.field(bits)
+    for a, b in zip(t, (F.log, F.exp, F.skew, F.walsh)):
+        assert np.array_equal(a.astype(np.int64), b.astype(np.int64))
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+def test_field_is_a_field(bits):
+    """exp/log are inverse bijections; mulLog distributes over XOR (linearity the kernels rely on)."""
+    F = lnp.field(bits)
+    n = F.order
+    assert np.array_equal(np.sort(F._log[1:]), np.arange(n - 1))
+    assert np.all(F._exp[F._log[1:]] == np.arange(1, n))
+    rng = np.random.default_rng(bits)
+    a = rng.integers(0, n, 2000)
+    b = rng.integers(0, n, 2000)
+    for lm in rng.integers(0, n, 20):
+        assert np.array_equal(F.mul_log(a ^ b, lm), F.mul_log(a, lm) ^ F.mul_log(b, lm))
+    # log 'modulus' is the identity for mulLog (leopard16.go:841-846)
+    assert np.array_equal(F.mul_log(a, F.mod), a)
+
+
+ENC = [(2, 1, 64), (4, 2, 128), (10, 4, 256), (5, 3, 64), (3, 7, 64), (16, 4, 192), (33, 17, 64),
+       (128, 32, 64), (100, 28, 64), (200, 100, 64), (70, 40, 64), (1, 1, 64), (300, 64, 64)]
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+@pytest.mark.parametrize("k,p,S", ENC)
+def test_encode_c_vs_numpy(bits, k, p, S):
+    if bits == 8 and k + p > 256:
+        pytest.skip("GF(2^8) codec is for <= 256 shards")
+    data = np.random.default_rng(k * 31 + p).integers(0, 256, (k, S), dtype=np.uint8)
+    assert np.array_equal(orc.encode(bits, k, p, data), lnp.encode(bits, k, p, data))
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+@pytest.mark.parametrize("k,p", [(4, 2), (10, 4), (16, 4), (20, 12), (33, 17), (128, 32), (5, 3)])
+def test_reconstruct_round_trip_all_classes(bits, k, p):
+    """testReconstruction (reedsolomon_test.go:195-310) over erasure classes:
+    data only, parity only, mixed, maximum (p) erasures; ReconstructData."""
+    S = 64
+    rng = np.random.default_rng(k + p)
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    par = orc.encode(bits, k, p, data)
+    full = [data[i] for i in range(k)] + [par[i] for i in range(p)]
+    patterns = [list(range(min(p, k))), list(range(k, k + p)), [0, k], rng.choice(k + p, p, replace=False).tolist()]
+    for er in patterns:
+        sh = [None if i in er else full[i].copy() for i in range(k + p)]
+        e, got = orc.Oracle(bits, k, p).reconstruct(sh, True)
+        assert e == 0
+        assert all(np.array_equal(got[i], full[i]) for i in range(k + p))
+        ref = lnp.reconstruct(bits, k, p, sh, True)
+        assert all(np.array_equal(ref[i], full[i]) for i in er)
+        e, got = orc.Oracle(bits, k, p).reconstruct([None if i in er else full[i].copy() for i in range(k + p)], False)
+        assert e == 0
+        for i in range(k + p):
+            if i < k:
+                assert np.array_equal(got[i], full[i])
+            elif i in er:
+                assert got[i] is None
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+def test_verify_and_errors(bits):
+    """testVerify (reedsolomon_test.go:313-411) and the sentinel errors."""
+    k, p, S = 10, 4, 128
+    data = np.random.default_rng(1).integers(0, 256, (k, S), dtype=np.uint8)
+    par = orc.encode(bits, k, p, data)
+    full = [data[i] for i in range(k)] + [par[i] for i in range(p)]
+    o = orc.Oracle(bits, k, p)
+    assert o.verify([x.copy() for x in full]) == (True, 0)
+    bad = [x.copy() for x in full]
+    bad[0][0] ^= 1
+    assert o.verify(bad) == (False, 0)
+    assert o.encode(full[:5]) == 3  # ErrTooFewShards
+    assert o.encode([x.copy() for x in full[:-1]] + [np.zeros(64, np.uint8)]) == 5  # ErrShardSize
+    odd = [np.zeros(65, np.uint8) for _ in range(k + p)]
+    assert o.encode(odd) == 6  # ErrInvalidShardSize
+    e, _ = o.reconstruct([None] * 5 + full[5:])
+    assert e == 3  # ErrTooFewShards (5 missing > p)
+    e, _ = o.reconstruct([None] * (k + p))
+    assert e == 4  # ErrShardNoData
+
+
+def test_reference_panics_are_modelled():
+    """GF(2^8) geometries whose skew slice runs past fftSkew8 (leopard8.go:167-206)."""
+    o = orc.Oracle(8, 129, 127)
+    sh = [np.zeros(64, np.uint8) for _ in range(256)]
+    assert o.encode(sh) == 50
+    # m + k > 256: the last encode chunk runs past fftSkew8 and reconstruct's
+    # errLocs[i+m] / fwht8 index past [256]ffe8.
+    o = orc.Oracle(8, 200, 40)
+    sh = [np.zeros(64, np.uint8) for _ in range(240)]
+    assert o.encode(sh) == 50
+    sh[0] = None
+    e, _ = o.reconstruct(sh)
+    assert e == 50
+    # m + k == 256 is fine for both
+    o = orc.Oracle(8, 128, 100)
+    sh = [np.zeros(64, np.uint8) for _ in range(228)]
+    assert o.encode(sh) == 0
+    sh[0] = None
+    e, _ = o.reconstruct(sh)
+    assert e == 0
+
+
+def test_gf8_inversion_cache_is_stateful():
+    """leopard8.go:508-555: the cache key is the data-erasure bitmap (parity
+    bits only when recoverAll), so a ReconstructData call can reuse error
+    locators computed for a different parity-erasure pattern.  The oracle
+    keeps that state per codec exactly as the reference does."""
+    k, p, S = 10, 4, 64
+    data = np.random.default_rng(2).integers(0, 256, (k, S), dtype=np.uint8)
+    par = orc.encode(8, k, p, data)
+    full = [data[i] for i in range(k)] + [par[i] for i in range(p)]
+    fresh = orc.Oracle(8, k, p)
+    e, ok = fresh.reconstruct([None if i in (0,) else full[i].copy() for i in range(k + p)], False)
+    assert e == 0 and np.array_equal(ok[0], full[0])
+    o = orc.Oracle(8, k, p)
+    e, _ = o.reconstruct([None if i in (0, k) else full[i].copy() for i in range(k + p)], False)
+    assert e == 0
+    e, second = o.reconstruct([None if i in (0,) else full[i].copy() for i in range(k + p)], False)
+    assert e == 0
+    # Same key {data 0}: the cached locators were computed with parity 0 erased.
+    assert not np.array_equal(second[0], full[0])
+
+
+def _load(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        return {key: z[key] for key in z.files}
+
+
+def golden_names():
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz"))
+
+
+def test_golden_manifest():
+    lines = open(os.path.join(GOLDEN, "MANIFEST.sha256")).read().split("\n")
+    want = dict(reversed(l.split("  ")) for l in lines if l.strip())
+    assert sorted(want) == sorted(n + ".npz" for n in golden_names())
+    for fn, h in want.items():
+        assert hashlib.sha256(open(os.path.join(GOLDEN, fn), "rb").read()).hexdigest() == h
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_fixtures(name):
+    g = _load(name)
+    bits, k, p = int(g["bits"][0]), int(g["k"][0]), int(g["p"][0])
+    assert np.array_equal(orc.encode(bits, k, p, g["data"]), g["parity"])
+    full = [g["data"][i] for i in range(k)] + [g["parity"][i] for i in range(p)]
+    for er in g["erasures"]:
+        sh = [None if er[i] else full[i].copy() for i in range(k + p)]
+        e, got = orc.Oracle(bits, k, p).reconstruct(sh, True)
+        assert e == 0 and all(np.array_equal(got[i], full[i]) for i in range(k + p))
