@@ -86,6 +86,23 @@ int rs_encode_idx(rs_codec *codec, const uint8_t *data_shard, size_t len, int id
 int rs_update(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards,
               uint8_t *const *new_data, const size_t *new_lens, int nnew);
 
+/* ---------------- Host-resident pipeline controls ---------------- */
+/* rs_encode / rs_verify / rs_reconstruct stream the stripe through the GPU in
+ * column segments (H2D, kernel and D2H on three streams, 3 staging slabs).
+ * Pinned host rows (rs_host_alloc / rs_host_register) make the copies true
+ * DMA; pageable rows work but are staged by the runtime.  Rows that are
+ * equally spaced (one AllocAligned-style slab) are copied with one 2-D copy
+ * per segment.  Segment width per row: `bytes` (multiple of 64) or 0 for
+ * automatic (about 8 MiB copied in per segment). */
+int rs_set_host_segment(rs_codec *codec, size_t bytes);
+/* Pinned, 64-byte-aligned host memory: AllocAligned (unsafe.go:17-41) for
+ * shards that are to cross PCIe at full rate. */
+int rs_host_alloc(size_t bytes, void **out);
+void rs_host_free(void *ptr);
+/* Pin existing host memory (e.g. a Go slab held by runtime.Pinner). */
+int rs_host_register(void *ptr, size_t bytes);
+int rs_host_unregister(void *ptr);
+
 /* ---------------- Device-resident entry points (HBM in, HBM out) ---------------- */
 /* d_shards: HOST array of k+p DEVICE pointers, each to shard_size bytes
  * (4-byte aligned; 64-byte aligned recommended).  stream: hipStream_t or NULL

@@ -21,11 +21,12 @@ from .codec import (  # noqa: F401
     ErrReconstructRequired,
     ErrPanic,
     ErrDevice,
+    alloc_pinned,
 )
 from ._capi import LIB_PATH, lib  # noqa: F401
 
 __all__ = [
     "New", "New8", "New16", "ReedSolomon", "RSError", "ErrInvShardNum", "ErrMaxShardNum", "ErrTooFewShards",
     "ErrShardNoData", "ErrShardSize", "ErrInvalidShardSize", "ErrNotSupported", "ErrShortData",
-    "ErrReconstructRequired", "ErrPanic", "ErrDevice", "LIB_PATH", "lib",
+    "ErrReconstructRequired", "ErrPanic", "ErrDevice", "LIB_PATH", "lib", "alloc_pinned",
 ]

@@ -38,6 +38,12 @@ def lib() -> C.CDLL:
     L.rs_verify_dev.argtypes = [vp, P(vp), sz, P(i32), vp]
     L.rs_reconstruct_dev.argtypes = [vp, P(vp), P(C.c_uint8), sz, i32, vp]
     L.rs_encode_dev_batch.argtypes = [vp, vp, sz, sz, i32, sz, vp]
+    L.rs_set_host_segment.argtypes = [vp, sz]
+    L.rs_host_alloc.argtypes = [sz, P(vp)]
+    L.rs_host_free.argtypes = [vp]
+    L.rs_host_free.restype = None
+    L.rs_host_register.argtypes = [vp, sz]
+    L.rs_host_unregister.argtypes = [vp]
     L.rs_encode_path.argtypes = [vp]
     L.rs_encode_path.restype = C.c_char_p
     L.rs_strerror.argtypes = [i32]

@@ -72,6 +72,31 @@ def _check(code: int) -> None:
 
 
 # --------------------------------------------------------------------------- helpers
+class _PinnedBlock:
+    """Owner of one rs_host_alloc block; freed when the last view dies."""
+
+    def __init__(self, nbytes: int):
+        L = _capi.lib()
+        p = C.c_void_p()
+        _check(L.rs_host_alloc(nbytes, C.byref(p)))
+        self.ptr, self._free = p.value, L.rs_host_free
+
+    def __del__(self):
+        if self.ptr:
+            self._free(self.ptr)
+            self.ptr = None
+
+
+def alloc_pinned(nbytes: int) -> np.ndarray:
+    """Page-locked, 64-byte-aligned host bytes (zeroed) as a numpy uint8 array."""
+    blk = _PinnedBlock(nbytes)
+    cbuf = (C.c_uint8 * nbytes).from_address(blk.ptr)
+    cbuf._owner = blk  # the ctypes buffer keeps the block alive; numpy keeps the buffer
+    a = np.frombuffer(cbuf, dtype=np.uint8)
+    a[:] = 0
+    return a
+
+
 def _host_rows(shards: Sequence):
     n = len(shards)
     ptrs = (C.c_void_p * n)()
@@ -171,14 +196,22 @@ class ReedSolomon:
     def encode_path(self) -> str:
         return self._L.rs_encode_path(self._h).decode()
 
-    def alloc_aligned(self, each: int, shards: Optional[int] = None):
-        """AllocAligned (unsafe.go:17-41): one 64-byte-aligned slab, rows of `each` bytes."""
+    def alloc_aligned(self, each: int, shards: Optional[int] = None, pinned: bool = False):
+        """AllocAligned (unsafe.go:17-41): one 64-byte-aligned slab, rows of `each` bytes.
+        pinned=True allocates page-locked memory (rs_host_alloc) so the host
+        pipeline's PCIe copies are DMA at full rate."""
         n = self.total_shards() if shards is None else shards
         each_al = (each + 63) // 64 * 64
-        raw = np.zeros(each_al * n + 64, dtype=np.uint8)
-        off = (-raw.ctypes.data) % 64
-        slab = raw[off:off + each_al * n]
+        slab = alloc_pinned(each_al * n) if pinned else None
+        if slab is None:
+            raw = np.zeros(each_al * n + 64, dtype=np.uint8)
+            off = (-raw.ctypes.data) % 64
+            slab = raw[off:off + each_al * n]
         return [slab[i * each_al:i * each_al + each] for i in range(n)]
+
+    def set_host_segment(self, nbytes: int) -> None:
+        """Column-segment width of the host pipeline (0 = automatic)."""
+        _check(self._L.rs_set_host_segment(self._h, nbytes))
 
     # ---------------- host-memory operations (Go [][]byte semantics)
     def encode(self, shards: list) -> None:

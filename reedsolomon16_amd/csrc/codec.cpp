@@ -27,6 +27,8 @@ using namespace rs;
 namespace {
 
 constexpr int kMaxRegLogM = 5;  // m <= 32: fused register kernel
+constexpr int kHostBufs = 3;    // staging slabs of the host-resident pipeline
+constexpr uint64_t kHostSegTarget = 8ull << 20;  // bytes copied in per segment
 
 template <class T>
 struct DevBuf {
@@ -90,7 +92,7 @@ struct rs_codec {
     DevBuf<uint32_t> dtw_ifft, dtw_fft;
 
     // scratch
-    DevBuf<uint8_t> work, slab;
+    DevBuf<uint8_t> work;
     DevBuf<uint8_t *> rows;         // row-pointer table (non-strided inputs)
     std::vector<uint8_t *> rows_host;
     DevBuf<int> flag;
@@ -102,13 +104,30 @@ struct rs_codec {
     // error-locator cache keyed by erasure pattern (bounded LRU)
     std::list<std::pair<std::vector<uint8_t>, std::vector<uint32_t>>> el_cache;
 
+    // host-resident pipeline (rs_encode / rs_verify / rs_reconstruct): copy-in,
+    // compute and copy-out streams over kHostBufs rotating staging slabs
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    hipEvent_t ev_in[kHostBufs] = {}, ev_k[kHostBufs] = {}, ev_free[kHostBufs] = {};
+    DevBuf<uint8_t> stage;
+    uint64_t host_seg_bytes = 0;  // 0: automatic
+
     ~rs_codec() {
         if (!dev_ready && !stream) return;
         DeviceGuard g(device);
         if (stream) (void)hipStreamSynchronize(stream);
         tw_ifft.release(); tw_fft.release(); dtw_ifft.release(); dtw_fft.release();
-        work.release(); slab.release(); rows.release(); flag.release();
+        work.release(); rows.release(); flag.release();
         rc_src.release(); rc_dst.release(); rc_tw_in.release(); rc_tw_out.release(); rc_pos.release();
+        if (s_in) (void)hipStreamSynchronize(s_in);
+        if (s_out) (void)hipStreamSynchronize(s_out);
+        stage.release();
+        for (int b = 0; b < kHostBufs; b++) {
+            if (ev_in[b]) (void)hipEventDestroy(ev_in[b]);
+            if (ev_k[b]) (void)hipEventDestroy(ev_k[b]);
+            if (ev_free[b]) (void)hipEventDestroy(ev_free[b]);
+        }
+        if (s_in) (void)hipStreamDestroy(s_in);
+        if (s_out) (void)hipStreamDestroy(s_out);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -263,9 +282,17 @@ const std::vector<uint32_t> *error_locs_cached(rs_codec *c, const std::vector<ui
     return &c->el_cache.front().second;
 }
 
-// Device reconstruct (leopard16.go:432-568) for already-validated input.
-int reconstruct_device(rs_codec *c, uint8_t *const *d, const std::vector<uint8_t> &present, uint64_t S,
-                       bool recover_all, hipStream_t s) {
+// Host half of a reconstruct (leopard16.go:432-568) for one erasure pattern:
+// which shard feeds each of the n work rows, the input scalings (errLocs),
+// which shards are rebuilt from which work row, and their output scalings.
+struct RecPlan {
+    std::vector<int> src_shard;   // n entries: shard index feeding work row r, or -1 (zero row)
+    std::vector<int> dst_shard;   // shards to rebuild, ascending
+    std::vector<int> pos;         // work row each rebuilt shard is read from
+    std::vector<uint32_t> tw_in, tw_out;
+};
+
+int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, RecPlan &pl) {
     int e = build_decode_plan(c);
     if (e) return e;
     if (!c->dec_ok) return RS_ERR_PANIC;
@@ -275,51 +302,82 @@ int reconstruct_device(rs_codec *c, uint8_t *const *d, const std::vector<uint8_t
     const std::vector<uint32_t> *elp = error_locs_cached(c, erased);
     if (!elp) return RS_ERR_PANIC;
     const std::vector<uint32_t> &el = *elp;
-
     // work rows: [recovery m][original k][zero to n] (leopard16.go:547)
-    std::vector<const uint8_t *> src(n, nullptr);
-    std::vector<uint32_t> tw_in((size_t)n * c->twd, 0);
+    pl.src_shard.assign(n, -1);
     for (int i = 0; i < p; i++)
-        if (present[k + i]) src[i] = d[k + i];
+        if (present[k + i]) pl.src_shard[i] = k + i;
     for (int i = 0; i < k; i++)
-        if (present[i]) src[m + i] = d[i];
+        if (present[i]) pl.src_shard[m + i] = i;
+    pl.tw_in.assign((size_t)n * c->twd, 0);
     for (int r = 0; r < m + k; r++)
-        if (src[r]) make_twiddle(*c->F, el[r], tw_in.data() + (size_t)r * c->twd);
-
-    std::vector<uint8_t *> dst;
-    std::vector<int> pos;
+        if (pl.src_shard[r] >= 0) make_twiddle(*c->F, el[r], pl.tw_in.data() + (size_t)r * c->twd);
+    pl.dst_shard.clear();
+    pl.pos.clear();
     const int end = recover_all ? total : k;
     for (int i = 0; i < end; i++) {
         if (present[i]) continue;
-        dst.push_back(d[i]);
-        pos.push_back(i >= k ? i - k : i + m);
+        pl.dst_shard.push_back(i);
+        pl.pos.push_back(i >= k ? i - k : i + m);
     }
-    std::vector<uint32_t> tw_out(std::max<size_t>(dst.size(), 1) * c->twd, 0);
-    for (size_t j = 0; j < dst.size(); j++)
-        make_twiddle(*c->F, (c->F->mod - el[pos[j]]) & c->F->mod, tw_out.data() + j * c->twd);
+    pl.tw_out.assign(std::max<size_t>(pl.dst_shard.size(), 1) * c->twd, 0);
+    for (size_t j = 0; j < pl.dst_shard.size(); j++)
+        make_twiddle(*c->F, (c->F->mod - el[pl.pos[j]]) & c->F->mod, pl.tw_out.data() + j * c->twd);
+    return RS_OK;
+}
 
-    HIP_TRY(c->work.ensure((size_t)n * S));
-    HIP_TRY(c->rc_src.ensure(n));
-    HIP_TRY(c->rc_tw_in.ensure(tw_in.size()));
-    HIP_TRY(c->rc_dst.ensure(std::max<size_t>(dst.size(), 1)));
-    HIP_TRY(c->rc_pos.ensure(std::max<size_t>(pos.size(), 1)));
-    HIP_TRY(c->rc_tw_out.ensure(tw_out.size()));
-    HIP_TRY(hipMemcpyAsync(c->rc_src.p, src.data(), n * sizeof(void *), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(c->rc_tw_in.p, tw_in.data(), tw_in.size() * 4, hipMemcpyHostToDevice, s));
-    if (!dst.empty()) {
-        HIP_TRY(hipMemcpyAsync(c->rc_dst.p, dst.data(), dst.size() * sizeof(void *), hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(c->rc_pos.p, pos.data(), pos.size() * sizeof(int), hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(c->rc_tw_out.p, tw_out.data(), tw_out.size() * 4, hipMemcpyHostToDevice, s));
+// Upload a plan for `nsets` row-pointer sets (set b: shard i at d[b][i]).
+// The host vectors must stay alive until the stream has consumed them.
+int upload_reconstruct(rs_codec *c, const RecPlan &pl, const std::vector<uint8_t *const *> &d,
+                       std::vector<const uint8_t *> &src_h, std::vector<uint8_t *> &dst_h, hipStream_t s) {
+    const int n = c->n, nd = (int)pl.dst_shard.size(), ns = (int)d.size();
+    src_h.assign((size_t)ns * n, nullptr);
+    dst_h.assign((size_t)ns * std::max(nd, 1), nullptr);
+    for (int b = 0; b < ns; b++) {
+        for (int r = 0; r < n; r++)
+            if (pl.src_shard[r] >= 0) src_h[(size_t)b * n + r] = d[b][pl.src_shard[r]];
+        for (int j = 0; j < nd; j++) dst_h[(size_t)b * std::max(nd, 1) + j] = d[b][pl.dst_shard[j]];
     }
+    HIP_TRY(c->rc_src.ensure(src_h.size()));
+    HIP_TRY(c->rc_dst.ensure(dst_h.size()));
+    HIP_TRY(c->rc_tw_in.ensure(pl.tw_in.size()));
+    HIP_TRY(c->rc_tw_out.ensure(pl.tw_out.size()));
+    HIP_TRY(c->rc_pos.ensure(std::max<size_t>(pl.pos.size(), 1)));
+    HIP_TRY(hipMemcpyAsync(c->rc_src.p, src_h.data(), src_h.size() * sizeof(void *), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->rc_dst.p, dst_h.data(), dst_h.size() * sizeof(void *), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->rc_tw_in.p, pl.tw_in.data(), pl.tw_in.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->rc_tw_out.p, pl.tw_out.data(), pl.tw_out.size() * 4, hipMemcpyHostToDevice, s));
+    if (!pl.pos.empty())
+        HIP_TRY(hipMemcpyAsync(c->rc_pos.p, pl.pos.data(), pl.pos.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    return RS_OK;
+}
+
+// Device work of one reconstruct over row-pointer set `set` of the uploaded plan.
+int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipStream_t s) {
+    const int n = c->n, nd = (int)pl.dst_shard.size();
+    HIP_TRY(c->work.ensure((size_t)n * S));
     uint8_t *w = c->work.p;
-    HIP_TRY(launch_scale_in(c->bits, w, S, c->rc_src.p, c->rc_tw_in.p, n, s));
-    e = run_passes(c, true, w, S, c->logn, m + k, c->dtw_ifft.p, s);
+    HIP_TRY(launch_scale_in(c->bits, w, S, c->rc_src.p + (size_t)set * n, c->rc_tw_in.p, n, s));
+    int e = run_passes(c, true, w, S, c->logn, c->m + c->k, c->dtw_ifft.p, s);
     if (e) return e;
     HIP_TRY(launch_formal_derivative(c->bits, w, S, n, s));
-    e = run_passes(c, false, w, S, c->logn, m + k, c->dtw_fft.p, s);
+    e = run_passes(c, false, w, S, c->logn, c->m + c->k, c->dtw_fft.p, s);
     if (e) return e;
-    if (!dst.empty())
-        HIP_TRY(launch_reveal(c->bits, c->rc_dst.p, w, S, c->rc_pos.p, c->rc_tw_out.p, (int)dst.size(), s));
+    if (nd) HIP_TRY(launch_reveal(c->bits, c->rc_dst.p + (size_t)set * nd, w, S, c->rc_pos.p, c->rc_tw_out.p, nd, s));
+    return RS_OK;
+}
+
+// Device reconstruct (leopard16.go:432-568) for already-validated input.
+int reconstruct_device(rs_codec *c, uint8_t *const *d, const std::vector<uint8_t> &present, uint64_t S,
+                       bool recover_all, hipStream_t s) {
+    RecPlan pl;
+    int e = plan_reconstruct(c, present, recover_all, pl);
+    if (e) return e;
+    std::vector<const uint8_t *> src_h;
+    std::vector<uint8_t *> dst_h;
+    e = upload_reconstruct(c, pl, {d}, src_h, dst_h, s);
+    if (e) return e;
+    e = launch_reconstruct(c, pl, 0, S, s);
+    if (e) return e;
     HIP_TRY(hipStreamSynchronize(s));  // host vectors above must outlive the async copies
     return RS_OK;
 }
@@ -338,9 +396,142 @@ int check_shards(const size_t *lens, int n, bool nilok) {
     return RS_OK;
 }
 
-int ensure_slab(rs_codec *c, uint64_t S, uint8_t **d) {
-    HIP_TRY(c->slab.ensure((size_t)c->total * S));
-    for (int i = 0; i < c->total; i++) d[i] = c->slab.p + (size_t)i * S;
+// ---------------------------------------------------------------- host-resident pipeline
+// Shards in host memory (the reference's own setting: Encode on [][]byte).
+// The stripe is cut into column segments (every operation is column-local,
+// leopard16.go:778-792); segment j is copied in on s_in, transformed on the
+// codec stream and copied out on s_out, through staging slab j % kHostBufs,
+// so PCIe copies in both directions overlap the kernels.
+
+int ensure_host_pipe(rs_codec *c) {
+    if (!c->s_in) HIP_TRY(hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking));
+    if (!c->s_out) HIP_TRY(hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
+    for (int b = 0; b < kHostBufs; b++) {
+        if (!c->ev_in[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_in[b], hipEventDisableTiming));
+        if (!c->ev_k[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_k[b], hipEventDisableTiming));
+        if (!c->ev_free[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_free[b], hipEventDisableTiming));
+    }
+    return RS_OK;
+}
+
+uint64_t host_segment(const rs_codec *c, uint64_t S, size_t in_rows) {
+    uint64_t seg = c->host_seg_bytes ? c->host_seg_bytes : kHostSegTarget / std::max<size_t>(in_rows, 1);
+    seg = std::max<uint64_t>(seg / 64 * 64, 64);
+    return std::min(seg, S);
+}
+
+// Copy bytes [off, off+w) of shards `rows` between host rows and a device slab
+// (shard i at dev + i*dpitch).  Runs of consecutive shards whose host rows are
+// equally spaced (an AllocAligned slab) go as one 2-D copy.
+int copy_rows(uint8_t *dev, uint64_t dpitch, uint8_t *const *host, const std::vector<int> &rows, uint64_t off,
+              uint64_t w, bool h2d, hipStream_t s) {
+    size_t i = 0;
+    while (i < rows.size()) {
+        size_t j = i + 1;
+        int64_t hp = 0;
+        if (j < rows.size() && rows[j] == rows[i] + 1) {
+            hp = (int64_t)(host[rows[j]] - host[rows[i]]);
+            if (hp >= (int64_t)w) {
+                while (j < rows.size() && rows[j] == rows[j - 1] + 1 &&
+                       (int64_t)(host[rows[j]] - host[rows[j - 1]]) == hp)
+                    j++;
+            } else {
+                j = i + 1;
+            }
+        }
+        uint8_t *d = dev + (uint64_t)rows[i] * dpitch;
+        uint8_t *h = host[rows[i]] + off;
+        if (j - i == 1) {
+            HIP_TRY(hipMemcpyAsync(h2d ? (void *)d : (void *)h, h2d ? (const void *)h : (const void *)d, w,
+                                   h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, s));
+        } else if (h2d) {
+            HIP_TRY(hipMemcpy2DAsync(d, dpitch, h, (size_t)hp, w, j - i, hipMemcpyHostToDevice, s));
+        } else {
+            HIP_TRY(hipMemcpy2DAsync(h, (size_t)hp, d, dpitch, w, j - i, hipMemcpyDeviceToHost, s));
+        }
+        i = j;
+    }
+    return RS_OK;
+}
+
+enum class HostOp { Encode, Verify, Reconstruct };
+
+int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, const std::vector<uint8_t> &present,
+                  bool recover_all, int *ok) {
+    int e = ensure_host_pipe(c);
+    if (e) return e;
+    hipStream_t sc = c->stream;
+    const int k = c->k, total = c->total;
+    std::vector<int> in_rows, out_rows;
+    RecPlan pl;
+    if (op == HostOp::Reconstruct) {
+        e = plan_reconstruct(c, present, recover_all, pl);
+        if (e) return e;
+        for (int i = 0; i < total; i++)
+            if (present[i]) in_rows.push_back(i);
+        out_rows = pl.dst_shard;
+    } else {
+        for (int i = 0; i < (op == HostOp::Verify ? total : k); i++) in_rows.push_back(i);
+        if (op == HostOp::Encode)
+            for (int i = k; i < total; i++) out_rows.push_back(i);
+    }
+    const uint64_t seg = host_segment(c, S, in_rows.size());
+    const uint64_t slab = (uint64_t)total * seg;
+    HIP_TRY(c->stage.ensure((size_t)kHostBufs * slab));
+    // scratch of the multi-pass paths, sized before any launch (no realloc mid-pipeline)
+    if (op == HostOp::Reconstruct) HIP_TRY(c->work.ensure((size_t)c->n * seg));
+    else if (c->logm > kMaxRegLogM) HIP_TRY(c->work.ensure((size_t)2 * c->m * seg));
+    std::vector<const uint8_t *> src_h;
+    std::vector<uint8_t *> dst_h;
+    std::vector<std::vector<uint8_t *>> sets(kHostBufs, std::vector<uint8_t *>(total));
+    if (op == HostOp::Reconstruct) {
+        std::vector<uint8_t *const *> d;
+        for (int b = 0; b < kHostBufs; b++) {
+            for (int i = 0; i < total; i++) sets[b][i] = c->stage.p + b * slab + (uint64_t)i * seg;
+            d.push_back(sets[b].data());
+        }
+        e = upload_reconstruct(c, pl, d, src_h, dst_h, sc);
+        if (e) return e;
+    }
+    if (op == HostOp::Verify) HIP_TRY(hipMemsetAsync(c->flag.p, 0, sizeof(int), sc));
+    // copies in must not start before this call's setup on the compute stream
+    HIP_TRY(hipEventRecord(c->ev_k[0], sc));
+    HIP_TRY(hipStreamWaitEvent(c->s_in, c->ev_k[0], 0));
+    const uint64_t nseg = (S + seg - 1) / seg;
+    for (uint64_t j = 0; j < nseg; j++) {
+        const int b = (int)(j % kHostBufs);
+        const uint64_t off = j * seg, w = std::min(seg, S - off);
+        uint8_t *st = c->stage.p + b * slab;
+        if (j >= (uint64_t)kHostBufs) HIP_TRY(hipStreamWaitEvent(c->s_in, c->ev_free[b], 0));
+        e = copy_rows(st, seg, shards, in_rows, off, w, true, c->s_in);
+        if (e) return e;
+        HIP_TRY(hipEventRecord(c->ev_in[b], c->s_in));
+        HIP_TRY(hipStreamWaitEvent(sc, c->ev_in[b], 0));
+        if (op == HostOp::Reconstruct) {
+            e = launch_reconstruct(c, pl, b, w, sc);
+        } else {
+            RowSet data{nullptr, st, seg}, par{nullptr, st + (uint64_t)k * seg, seg};
+            e = encode_device(c, data, par, w, 0, 1, op == HostOp::Verify ? c->flag.p : nullptr, sc);
+        }
+        if (e) return e;
+        HIP_TRY(hipEventRecord(c->ev_k[b], sc));
+        if (!out_rows.empty()) {
+            HIP_TRY(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0));
+            e = copy_rows(st, seg, shards, out_rows, off, w, false, c->s_out);
+            if (e) return e;
+            HIP_TRY(hipEventRecord(c->ev_free[b], c->s_out));
+        } else {
+            HIP_TRY(hipEventRecord(c->ev_free[b], sc));
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(c->s_in));
+    HIP_TRY(hipStreamSynchronize(sc));
+    HIP_TRY(hipStreamSynchronize(c->s_out));
+    if (op == HostOp::Verify) {
+        int h = 1;
+        HIP_TRY(hipMemcpy(&h, c->flag.p, sizeof(int), hipMemcpyDeviceToHost));
+        *ok = h == 0;
+    }
     return RS_OK;
 }
 
@@ -471,21 +662,12 @@ int rs_encode(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshar
     const uint64_t S = shard_size_of(lens, nshards);
     if (S % 64) return RS_ERR_INVALID_SHARD_SIZE;
     if (!c->enc_ok) return RS_ERR_PANIC;
+    for (int i = 0; i < nshards; i++)
+        if (!shards[i]) return RS_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (int ie = ensure_device(c)) return ie;
-    hipStream_t s = c->stream;
-    std::vector<uint8_t *> d(c->total);
-    e = ensure_slab(c, S, d.data());
-    if (e) return e;
-    for (int i = 0; i < c->k; i++) HIP_TRY(hipMemcpyAsync(d[i], shards[i], S, hipMemcpyHostToDevice, s));
-    RowSet data{nullptr, d[0], S}, par{nullptr, d[c->k], S};
-    e = encode_device(c, data, par, S, 0, 1, nullptr, s);
-    if (e) return e;
-    for (int i = 0; i < c->p; i++)
-        HIP_TRY(hipMemcpyAsync(shards[c->k + i], d[c->k + i], S, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    return RS_OK;
+    return host_pipeline(c, shards, S, HostOp::Encode, {}, true, nullptr);
 }
 
 int rs_verify(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshards, int *ok) {
@@ -497,23 +679,12 @@ int rs_verify(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshar
     const uint64_t S = lens[0];
     if (S % 64) return RS_ERR_INVALID_SHARD_SIZE;
     if (!c->enc_ok) return RS_ERR_PANIC;
+    for (int i = 0; i < nshards; i++)
+        if (!shards[i]) return RS_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (int ie = ensure_device(c)) return ie;
-    hipStream_t s = c->stream;
-    std::vector<uint8_t *> d(c->total);
-    e = ensure_slab(c, S, d.data());
-    if (e) return e;
-    for (int i = 0; i < c->total; i++) HIP_TRY(hipMemcpyAsync(d[i], shards[i], S, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(c->flag.p, 0, sizeof(int), s));
-    RowSet data{nullptr, d[0], S}, par{nullptr, d[c->k], S};
-    e = encode_device(c, data, par, S, 0, 1, c->flag.p, s);
-    if (e) return e;
-    int h = 1;
-    HIP_TRY(hipMemcpyAsync(&h, c->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    *ok = h == 0;
-    return RS_OK;
+    return host_pipeline(c, shards, S, HostOp::Verify, {}, true, ok);
 }
 
 int rs_reconstruct(rs_codec *c, uint8_t *const *shards, size_t *lens, int nshards, int recover_all) {
@@ -532,28 +703,47 @@ int rs_reconstruct(rs_codec *c, uint8_t *const *shards, size_t *lens, int nshard
     const uint64_t S = shard_size_of(lens, nshards);
     if (S % 64) return RS_ERR_INVALID_SHARD_SIZE;
     const int end = recover_all ? c->total : c->k;
-    for (int i = 0; i < end; i++)
-        if (!lens[i] && !shards[i]) return RS_ERR_INVALID_ARG;
+    for (int i = 0; i < c->total; i++)
+        if ((lens[i] || i < end) && !shards[i]) return RS_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (int ie = ensure_device(c)) return ie;
-    hipStream_t s = c->stream;
-    std::vector<uint8_t *> d(c->total);
-    e = ensure_slab(c, S, d.data());
-    if (e) return e;
     std::vector<uint8_t> pr(c->total);
-    for (int i = 0; i < c->total; i++) {
-        pr[i] = lens[i] != 0;
-        if (pr[i]) HIP_TRY(hipMemcpyAsync(d[i], shards[i], S, hipMemcpyHostToDevice, s));
-    }
-    e = reconstruct_device(c, d.data(), pr, S, recover_all != 0, s);
+    for (int i = 0; i < c->total; i++) pr[i] = lens[i] != 0;
+    e = host_pipeline(c, shards, S, HostOp::Reconstruct, pr, recover_all != 0, nullptr);
     if (e) return e;
-    for (int i = 0; i < end; i++) {
-        if (pr[i]) continue;
-        HIP_TRY(hipMemcpyAsync(shards[i], d[i], S, hipMemcpyDeviceToHost, s));
-        lens[i] = S;
-    }
-    HIP_TRY(hipStreamSynchronize(s));
+    for (int i = 0; i < end; i++)
+        if (!pr[i]) lens[i] = S;
+    return RS_OK;
+}
+
+int rs_set_host_segment(rs_codec *c, size_t bytes) {
+    if (!c || bytes % 64) return RS_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->host_seg_bytes = bytes;
+    return RS_OK;
+}
+
+int rs_host_alloc(size_t bytes, void **out) {
+    if (!out || bytes == 0) return RS_ERR_INVALID_ARG;
+    *out = nullptr;
+    HIP_TRY(hipHostMalloc(out, bytes, hipHostMallocPortable));
+    return RS_OK;
+}
+
+void rs_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int rs_host_register(void *p, size_t bytes) {
+    if (!p || bytes == 0) return RS_ERR_INVALID_ARG;
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterPortable));
+    return RS_OK;
+}
+
+int rs_host_unregister(void *p) {
+    if (!p) return RS_ERR_INVALID_ARG;
+    HIP_TRY(hipHostUnregister(p));
     return RS_OK;
 }
 

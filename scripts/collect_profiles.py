@@ -1,0 +1,95 @@
+"""Copy the round's GPU evidence from gpurun_out/round into profiles/.
+
+Writes profiles/rNN_bench.json, rNN_kernel_stats.csv (rocprofv3 --stats,
+kernel names shortened), rNN_pmc.txt and profiles/pmc_traffic.json, which
+bench.py reads for roofline.traffic.  HBM bytes per launch =
+2 * FETCH_SIZE + WRITE_SIZE (rocprofv3 reports KiB; gfx950 FETCH_SIZE counts
+half of a wide coalesced streaming read, MI355X_MICROARCH.md "HBM")."""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name: str) -> str:
+    if "rs::" not in name:
+        return re.split(r"[<(]", name.replace("void ", ""), 1)[0][:80]
+    return name.replace("void ", "").replace("rs::(anonymous namespace)::", "").replace("(rs::EncodeArgs)", "")
+
+
+def path_of(name: str):
+    """k_encode_reg<F16<W>, LOGM, VERIFY, TABLE> -> the engine's path name (codec.cpp)."""
+    m = re.search(r"k_encode_reg<rs::\(anonymous namespace\)::F(16|8)<\d+>, (\d+), (false|true)", name)
+    if not m:
+        return None
+    return f"reg{m.group(1)}-m{1 << int(m.group(2))}" + ("-verify" if m.group(3) == "true" else "")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--round", type=int, required=True)
+    ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out", "round"))
+    a = ap.parse_args()
+    tag = f"r{a.round:02d}"
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+
+    with open(os.path.join(a.src, "bench.json")) as f:
+        bench = json.loads([l for l in f if l.startswith("{")][-1])
+    with open(os.path.join(prof, f"{tag}_bench.json"), "w") as f:
+        json.dump(bench, f, indent=1)
+
+    rows = list(csv.DictReader(open(os.path.join(a.src, "trace", "run_kernel_stats.csv"))))
+    with open(os.path.join(prof, f"{tag}_kernel_stats.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+        w.writeheader()
+        for r in rows:
+            r = dict(r)
+            r["Name"] = short(r["Name"])
+            w.writerow(r)
+
+    agg = collections.defaultdict(list)
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        for fn in glob.glob(os.path.join(a.src, f"pmc_{c}", "run_counter_collection.csv")):
+            for r in csv.DictReader(open(fn)):
+                p = path_of(r["Kernel_Name"])
+                if p:
+                    agg[(p, r["Counter_Name"])].append(float(r["Counter_Value"]))
+    traffic, lines = {}, []
+    for p in sorted({k[0] for k in agg}):
+        fk = agg.get((p, "FETCH_SIZE"), [])
+        wk = agg.get((p, "WRITE_SIZE"), [])
+        if not fk or not wk:
+            continue
+        fetch = sum(fk) / len(fk) * 1024
+        write = sum(wk) / len(wk) * 1024
+        hbm = 2 * fetch + write
+        traffic[p] = {"hbm_bytes_per_launch": round(hbm), "fetch_size_bytes": round(fetch),
+                      "write_size_bytes": round(write), "launches": len(fk),
+                      "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE = half of streamed reads)",
+                      "round": tag}
+        lines.append(f"{p}: FETCH_SIZE {fetch/1e6:.2f} MB (x2 = {2*fetch/1e6:.2f}), WRITE_SIZE {write/1e6:.2f} MB, "
+                     f"HBM {hbm/1e6:.2f} MB/launch over {len(fk)} launches")
+    kern = [r for r in rows if "k_encode" in r["Name"]]
+    for r in kern:
+        lines.append(f"trace {short(r['Name'])}: calls {r['Calls']} avg {float(r['AverageNs'])/1e3:.2f} us "
+                     f"min {float(r['MinNs'])/1e3:.2f} max {float(r['MaxNs'])/1e3:.2f}")
+    lines.append(f"bench kernel_ms (HIP events) {bench['roofline']['kernel_ms']*1e3:.2f} us, "
+                 f"achieved {bench['roofline']['achieved']} GB/s, frac {bench['roofline']['frac']}")
+    with open(os.path.join(prof, f"{tag}_pmc.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    tpath = os.path.join(prof, "pmc_traffic.json")
+    old = json.load(open(tpath)) if os.path.exists(tpath) else {}
+    old.update(traffic)
+    with open(tpath, "w") as f:
+        json.dump(old, f, indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,50 @@ CONFIGS = {
     "C5": (16, 1024, 256, 256 << 10, "encode"),
     "C5x8": (16, 1024, 256, 32 << 10, "encode"),
 }
+# Host-resident (PCIe-inclusive) variants: shards in host memory, rs_encode /
+# rs_reconstruct stream them through the GPU.  "p" = pinned rows (rs_host_alloc).
+HOST_CONFIGS = {
+    "H3": (16, 128, 32, 1 << 20, "encode", False),
+    "H3p": (16, 128, 32, 1 << 20, "encode", True),
+    "H4p": (16, 128, 32, 1 << 20, "reconstruct", True),
+    "H3vp": (16, 128, 32, 1 << 20, "verify", True),
+}
+
+
+def time_host(name, iters, tag):
+    import time
+
+    import numpy as np
+
+    import reedsolomon16_amd as rs
+
+    bits, k, p, S, op, pinned = HOST_CONFIGS[name]
+    c = rs.ReedSolomon(k, p, bits)
+    shards = c.alloc_aligned(S, pinned=pinned)
+    rng = np.random.default_rng(1)
+    for i in range(k):
+        shards[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+    c.encode(shards)
+    er = set(rng.choice(k + p, p, replace=False).tolist())
+
+    def run():
+        if op == "encode":
+            c.encode(shards)
+        elif op == "verify":
+            assert c.verify(shards)
+        else:
+            c.reconstruct([np.zeros(0, np.uint8) if i in er else shards[i] for i in range(k + p)])
+
+    for _ in range(3):
+        run()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        run()
+    us = (time.perf_counter() - t0) / iters * 1e6
+    moved = {"encode": (k + p) * S, "verify": (k + p) * S, "reconstruct": (k + p) * S}[op]
+    print(json.dumps({"tag": tag, "config": name, "op": op, "pinned": pinned, "us": round(us, 1),
+                      "data_GiBps": round(k * S / us * 1e6 / 2**30, 2),
+                      "pcie_GBps": round(moved / us / 1e3, 1)}), flush=True)
 
 
 def main():
@@ -29,6 +73,9 @@ def main():
     import reedsolomon16_amd as rs
 
     for name in a.configs.split(","):
+        if name in HOST_CONFIGS:
+            time_host(name, max(5, a.iters // 5), a.tag)
+            continue
         bits, k, p, S, op = CONFIGS[name]
         c = rs.ReedSolomon(k, p, bits)
         slab = torch.randint(0, 256, (1, k + p, S), dtype=torch.uint8, device="cuda")

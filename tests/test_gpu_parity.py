@@ -293,3 +293,55 @@ def test_byte_range_sharding_on_gpu(torch_dev, bits, k, p, S, world):
         rsd.reconstruct_sharded(broken, present, r, world, rsd.gpu_reconstruct_fn(c))
     torch.cuda.synchronize()
     assert torch.equal(broken, whole)
+
+
+# Host-resident pipeline (rs_encode / rs_verify / rs_reconstruct): small
+# segment widths force many segments, a ragged last segment and reuse of every
+# staging slab; rows as one slab (2-D copies) and as scattered arrays
+# (per-row copies); pinned and pageable memory.
+@pytest.mark.parametrize("bits,k,p,S,seg", [(16, 128, 32, 64 * 37, 256), (16, 10, 4, 64 * 50, 640),
+                                            (8, 10, 4, 64 * 33, 128), (16, 300, 64, 64 * 9, 128),
+                                            (8, 100, 28, 64 * 20, 64 * 7)])
+@pytest.mark.parametrize("layout", ["slab", "scattered", "pinned"])
+def test_host_pipeline_segments(bits, k, p, S, seg, layout):
+    rng = np.random.default_rng(S + seg + k)
+    data = rand_data(rng, k, S)
+    ref = orc.encode(bits, k, p, data)
+    c = rs.ReedSolomon(k, p, bits)
+    c.set_host_segment(seg)
+    if layout == "scattered":
+        shards = [np.ascontiguousarray(data[i]) for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+    else:
+        shards = c.alloc_aligned(S, pinned=(layout == "pinned"))
+        for i in range(k):
+            shards[i][:] = data[i]
+    c.encode(shards)
+    assert np.array_equal(np.stack(shards[k:]), ref)
+    assert c.verify(shards)
+    shards[k + p - 1][S - 1] ^= 0x40  # last byte of the last segment
+    assert not c.verify(shards)
+    shards[k + p - 1][S - 1] ^= 0x40
+    er = set(rng.choice(k + p, p, replace=False).tolist())
+    # missing = nil (scattered) or an empty view (slab); rebuilt rows come back as fresh arrays
+    gone = None if layout == "scattered" else np.zeros(0, np.uint8)
+    broken = [gone if i in er else shards[i] for i in range(k + p)]
+    out = c.reconstruct(broken)
+    full = np.concatenate([data, ref])
+    for i in range(k + p):
+        assert np.array_equal(out[i], full[i]), i
+
+
+def test_host_pipeline_c3_pinned_matches_device(torch_dev):
+    torch = torch_dev
+    k, p, S = 128, 32, 1 << 20
+    c = rs.New16(k, p)
+    shards = c.alloc_aligned(S, pinned=True)
+    rng = np.random.default_rng(77)
+    for i in range(k):
+        shards[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+    c.encode(shards)
+    dev = torch.from_numpy(np.stack(shards[:k] + [np.zeros(S, np.uint8)] * p)).cuda()
+    c.encode_dev(dev)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev[k:].cpu().numpy(), np.stack(shards[k:]))
+    assert c.verify(shards)
