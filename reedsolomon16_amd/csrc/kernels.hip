@@ -42,13 +42,19 @@
 #define RS_STAMP 0
 #endif
 #if RS_STAMP
-__device__ unsigned long long g_rs_stamps[1 << 16];
+__device__ unsigned long long g_rs_stamps[3 << 16];
 #endif
 // RS_OP_FENCE: scheduling fence after every butterfly op of the fused kernels.
 #ifndef RS_OP_FENCE
 #define RS_OP_FENCE 0
 #endif
 // RS_OP_PIN: chain every butterfly op's outputs with an empty asm (bounds code motion).
+#ifndef RS_ABL_IFFT_AS_FFT
+#define RS_ABL_IFFT_AS_FFT 0  // timing experiment only: run the FFT op list per chunk (wrong result)
+#endif
+#ifndef RS_DMA_SPREAD
+#define RS_DMA_SPREAD 1
+#endif
 #ifndef RS_OP_PIN
 #define RS_OP_PIN 1
 #endif
@@ -441,8 +447,14 @@ struct TabRuns {
 // tables ahead of use; scheduling fences keep each load at the top of its
 // region (the machine scheduler would otherwise sink it next to its wait)
 // and bound the VGPR pressure of the fully unrolled code.
-template <class F, class OPS>
-__device__ __forceinline__ void run_ops(typename F::Vec *w, uint32_t ltab) {
+struct NoHook {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+
+// hook(i) runs before op i (i is a constant after unrolling): lets the caller
+// spread other issue work, e.g. the next chunk's LDS-DMAs, through the ops.
+template <class F, class OPS, class Hook = NoHook>
+__device__ __forceinline__ void run_ops(typename F::Vec *w, uint32_t ltab, const Hook &hook = Hook{}) {
     constexpr OPS ops{};
     constexpr TabRuns<OPS> runs{};
     constexpr int N = OPS::N;
@@ -455,6 +467,7 @@ __device__ __forceinline__ void run_ops(typename F::Vec *w, uint32_t ltab) {
     for (int i = 0; i < N; i++) {
         const BOp o = ops.op[i];
         const int need = runs.first_use[i];
+        hook(i);
         if (!RS_ABL_TAB_ONCE && need >= 0 && need != have) {  // next run: its table was prefetched into t1
             t0 = t1;
             have = need;
@@ -484,9 +497,14 @@ __device__ __forceinline__ void run_ops(typename F::Vec *w, uint32_t ltab) {
     }
 }
 
-template <class F, int LOGM>
-__device__ __forceinline__ void ifft_reg(typename F::Vec (&w)[1 << LOGM], uint32_t ltab) {
-    if constexpr (LOGM > 0) run_ops<F, IfftOps<LOGM>>(w, ltab);
+template <class F, int LOGM, class Hook = NoHook>
+__device__ __forceinline__ void ifft_reg(typename F::Vec (&w)[1 << LOGM], uint32_t ltab, const Hook &hook = Hook{}) {
+    if constexpr (LOGM > 0) run_ops<F, IfftOps<LOGM>, Hook>(w, ltab, hook);
+}
+template <int LOGM>
+constexpr int ifft_op_count() {
+    if constexpr (LOGM > 0) return IfftOps<LOGM>::N;
+    return 0;
 }
 template <class F, int LOGM>
 __device__ __forceinline__ void fft_reg(typename F::Vec (&w)[1 << LOGM], uint32_t ltab) {
@@ -508,6 +526,13 @@ __device__ __forceinline__ uint32_t vgpr_lds_addr(const uint8_t *p) {
     asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(a));
     return v;
 }
+
+// Waits through the builtin, not inline asm: the waitcnt-insertion pass sees
+// them and resets its model, so later LDS table reads get graded
+// lgkmcnt(N) waits (prefetch kept in flight) instead of lgkmcnt(0).
+// gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8].
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 
 template <bool TABLE>
 __device__ __forceinline__ uint8_t *rowp(const RowSet &rs, int i, uint64_t soff) {
@@ -549,30 +574,48 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
 
     // Stage chunk c's rows: rows past the chunk's count and pieces past the
     // row end are zero-filled.
-    auto stage = [&](int c) {
+    // Buffer descriptor over this stripe's data rows (strided mode; the host
+    // guarantees (k-1)*stride + shard_size < 2^32).
+    const __amdgpu_buffer_rsrc_t drsrc = __builtin_amdgcn_make_buffer_rsrc(
+        TABLE ? nullptr : (void *)(a.data.base + soff), 0,
+        TABLE ? 0 : (int)(uint32_t)((uint64_t)(a.k - 1) * a.data.stride + a.shard_size), 0x00020000);
+    // One DMA wave-instruction (piece group j) of chunk c's rows.
+    auto stage_one = [&](int c, int j) {
         const int row0 = c * M, cnt = a.k - row0;
-#pragma unroll
-        for (int j = 0; j < NDMA; j++) {
+        {
             const int P = j * 64 + lane;
             const int r = P / PPR;
             const uint64_t go = span + F::piece_goff(P % PPR);
             if (RS_ABL_NO_DMA) {
             } else if (wave_live && r < cnt && go < a.shard_size) {
-                const uint8_t *src = rowp<TABLE>(a.data, row0 + r, soff) + go;
-                __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(img + j * 1024), 16, 0, 0);
+                if constexpr (TABLE) {
+                    const uint8_t *src = rowp<TABLE>(a.data, row0 + r, soff) + go;
+                    __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(img + j * 1024), 16, 0, 0);
+                } else {
+                    // MUBUF LDS-DMA: with a FLAT global_load_lds in flight the compiler's
+                    // waitcnt model turns every LDS table wait into lgkmcnt(0).
+                    const uint32_t voff = (uint32_t)((uint64_t)(row0 + r) * a.data.stride + go);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(drsrc, (lvoid_t *)(img + j * 1024), 16, voff, 0, 0, 0);
+                }
             } else {
                 *(__attribute__((address_space(3))) u32x4 *)(img + j * 1024 + lane * 16) = u32x4{0, 0, 0, 0};
             }
         }
     };
+    auto stage = [&](int c) {
+#pragma unroll
+        for (int j = 0; j < NDMA; j++) stage_one(c, j);
+    };
+
     // Stage `nslot` twiddle tables into table buffer b (waves split the pieces).
     auto stage_tab = [&](const uint32_t *src, int nslot, int b) {
         const int npieces = nslot * TB / 16;
         const int P = wave * 64 + lane;
+        const __amdgpu_buffer_rsrc_t trsrc = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, npieces * 16, 0x00020000);
         for (int base = 0; base < npieces; base += 256) {
             if (base + P < npieces)
-                __builtin_amdgcn_global_load_lds((gvoid_t *)((const uint8_t *)src + (base + P) * 16),
-                                                 (lvoid_t *)(ltab + b * TABB + base * 16 + wave * 1024), 16, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(trsrc, (lvoid_t *)(ltab + b * TABB + base * 16 + wave * 1024),
+                                                         16, (base + P) * 16, 0, 0, 0);
         }
     };
 
@@ -589,7 +632,7 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
 #if RS_STAMP
         const unsigned long long sw0 = __builtin_amdgcn_s_memtime();
 #endif
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs for chunk c have landed
+        wait_vm0();  // this wave's DMAs for chunk c have landed
         __syncthreads();  // every wave's table pieces landed; buffer (c+1)&1 is no longer read
 #if RS_STAMP
         {
@@ -601,14 +644,24 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
         V cur[M];
 #pragma unroll
         for (int r = 0; r < M; r++) cur[r] = F::lds_load(img + r * ROWB, lane);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the image is overwritten
-        if (c + 1 < a.nchunks) {
-            stage(c + 1);
-            stage_tab(a.tw_ifft + (uint64_t)(c + 1) * IS * F::TWD, IS, (c + 1) & 1);
+        wait_lgkm0();  // reads done before the image is overwritten
+        const bool more = c + 1 < a.nchunks;
+        if (more) stage_tab(a.tw_ifft + (uint64_t)(c + 1) * IS * F::TWD, IS, (c + 1) & 1);
+        else stage_tab(a.tw_fft, FS, (c + 1) & 1);
+        // The next chunk's row DMAs are issued spread through the IFFT (one
+        // every SPREAD ops): issued back to back while the whole GPU streams,
+        // they stall the wave at issue before any butterfly starts.
+        constexpr int NOPS = ifft_op_count<LOGM>();
+        constexpr int SPREAD = (RS_DMA_SPREAD && NOPS >= NDMA) ? NOPS / NDMA : 0;
+        if (!SPREAD && more) stage(c + 1);
+        if (RS_ABL_IFFT_AS_FFT) {
+            if (more) stage(c + 1);
+            fft_reg<F, LOGM>(cur, vgpr_lds_addr(ltab + (c & 1) * TABB));
         } else {
-            stage_tab(a.tw_fft, FS, (c + 1) & 1);
+            ifft_reg<F, LOGM>(cur, vgpr_lds_addr(ltab + (c & 1) * TABB), [&](int i) {
+                if (SPREAD && i % SPREAD == 0 && i / SPREAD < NDMA && more) stage_one(c + 1, i / SPREAD);
+            });
         }
-        ifft_reg<F, LOGM>(cur, vgpr_lds_addr(ltab + (c & 1) * TABB));
         if (c == 0) {
 #pragma unroll
             for (int r = 0; r < M; r++) acc[r] = cur[r];
@@ -616,11 +669,20 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
 #pragma unroll
             for (int r = 0; r < M; r++) F::xor_into(acc[r], cur[r]);
         }
+#if RS_STAMP
+        if (lane == 0 && blockIdx.y == 0 && c < 8) {
+            const unsigned i3 = (blockIdx.x * 4 + wave) * 16 + 2 * c + 65536;
+            if (i3 + 1 < 3u * 65536) {
+                g_rs_stamps[i3] = __builtin_amdgcn_s_memtime() - sw0;  // whole chunk incl. wait
+                g_rs_stamps[i3 + 1] = sw0 - st_c0;                      // chunk start
+            }
+        }
+#endif
     }
 #if RS_STAMP
     const unsigned long long sf0 = __builtin_amdgcn_s_memtime();
 #endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_vm0();
     __syncthreads();
 #if RS_STAMP
     const unsigned long long sf1 = __builtin_amdgcn_s_memtime();

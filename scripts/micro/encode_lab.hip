@@ -27,7 +27,7 @@ int main(int argc, char **argv) {
     (void)hipEventSynchronize(e1);
     float ms;
     (void)hipEventElapsedTime(&ms, e0, e1);
-    std::vector<unsigned long long> st(1 << 16);
+    std::vector<unsigned long long> st(3 << 16);
     (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_rs_stamps), st.size() * 8);
     double cyc = 0, rt = 0;
     int n = 0;
@@ -58,6 +58,15 @@ int main(int argc, char **argv) {
     }
     printf("per wave (cycles): first-data wait %.0f | later chunk waits %.0f | IFFT phase total %.0f | FFT %.0f | after FFT %.0f\n",
            f / 2048, wt / 2048, pre / 2048 - f / 2048 - wt / 2048, fft / 2048, cyc - pre / 2048 - fft / 2048);
+    double ch[8] = {0}, cs[8] = {0};
+    for (int w = 0; w < 2048; w++)
+        for (int c = 0; c < 4; c++) {
+            ch[c] += st[65536 + 16 * w + 2 * c];
+            cs[c] += st[65536 + 16 * w + 2 * c + 1];
+        }
+    printf("per chunk (cycles, incl. its top wait): ");
+    for (int c = 0; c < 4; c++) printf(" c%d start %.0f dur %.0f |", c, cs[c] / 2048, ch[c] / 2048);
+    printf("\n");
     unsigned long long hw0 = st[3];
     printf("sample hw_id/xcc of wave0: xcc=%llu hwid=0x%llx\n", hw0 >> 32, hw0 & 0xffffffffull);
     printf("kernel %.2f us/launch; waves %d; mean wave life %.0f shader cycles = %.2f us; clock %.3f GHz\n",
