@@ -136,6 +136,15 @@ int rs_debug_twiddle_dwords(int field_bits);
 int rs_debug_error_locators(int field_bits, int data_shards, int parity_shards, const uint8_t *erased,
                             uint32_t *out);
 
+/* Checks the half-wave split schedules of the GF(2^16) encode kernel
+ * (logm 2..5) against the plain butterfly order on random symbols and
+ * twiddles, on the host.  Returns the number of differing rows (0 = equal). */
+int rs_debug_split_check(int logm, uint32_t seed);
+/* Host emulation of the split encode kernel's data flow (same twiddle images,
+ * byte-permute multiply and half-wave layout): data = k rows of S bytes,
+ * parity = p rows of S bytes.  GF(2^16) codecs with 4 <= m <= 32 only. */
+int rs_debug_split_emulate(rs_codec *codec, const uint8_t *data, uint8_t *parity, size_t shard_size);
+
 /* Human-readable message for an error code. */
 const char *rs_strerror(int code);
 

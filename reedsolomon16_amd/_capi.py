@@ -52,6 +52,8 @@ def lib() -> C.CDLL:
     L.rs_debug_twiddle.argtypes = [i32, C.c_uint32, vp]
     L.rs_debug_twiddle_dwords.argtypes = [i32]
     L.rs_debug_error_locators.argtypes = [i32, i32, i32, vp, vp]
+    L.rs_debug_split_check.argtypes = [i32, C.c_uint32]
+    L.rs_debug_split_emulate.argtypes = [vp, vp, vp, sz]
     _lib = L
     return L
 

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <list>
 #include <map>
@@ -21,6 +22,7 @@
 #include "../../include/rs_mi355x.h"
 #include "gf_host.hpp"
 #include "kernels.hpp"
+#include "schedule.hpp"
 
 using namespace rs;
 
@@ -84,6 +86,8 @@ struct rs_codec {
     int nchunks = 0;
     std::vector<uint32_t> enc_ifft_logs, enc_fft_logs;
     DevBuf<uint32_t> tw_ifft, tw_fft;
+    bool split_ok = false;            // half-wave split kernel available (GF(2^16), 4 <= m <= 32)
+    DevBuf<uint32_t> tws_ifft, tws_fft;  // its twiddle images (schedule.hpp EncodeSplit)
     std::string path;
 
     // decode plan (built on first reconstruct)
@@ -115,7 +119,7 @@ struct rs_codec {
         if (!dev_ready && !stream) return;
         DeviceGuard g(device);
         if (stream) (void)hipStreamSynchronize(stream);
-        tw_ifft.release(); tw_fft.release(); dtw_ifft.release(); dtw_fft.release();
+        tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); dtw_ifft.release(); dtw_fft.release();
         work.release(); rows.release(); flag.release();
         rc_src.release(); rc_dst.release(); rc_tw_in.release(); rc_tw_out.release(); rc_pos.release();
         if (s_in) (void)hipStreamSynchronize(s_in);
@@ -143,10 +147,66 @@ int upload_twiddles(rs_codec *c, const std::vector<uint32_t> &logs, DevBuf<uint3
     return RS_OK;
 }
 
+// ---- half-wave split kernel: table layout from the same compile-time schedule
+struct SplitTabs {
+    std::vector<int> lo, hi;  // twiddle slot per table load (-1: zero table)
+};
+template <class S>
+void split_tabs_of(const S &s, SplitTabs &t) {
+    t.lo.assign(s.tab_lo, s.tab_lo + s.ntab);
+    t.hi.assign(s.tab_hi, s.tab_hi + s.ntab);
+}
+template <int L>
+void split_tabs_t(bool fft, SplitTabs &t) {
+    if (fft) split_tabs_of(EncodeSplit<L>::fft, t);
+    else split_tabs_of(EncodeSplit<L>::ifft, t);
+}
+bool split_tabs(int logm, bool fft, SplitTabs &t) {
+    switch (logm) {
+        case 2: split_tabs_t<2>(fft, t); return true;
+        case 3: split_tabs_t<3>(fft, t); return true;
+        case 4: split_tabs_t<4>(fft, t); return true;
+        case 5: split_tabs_t<5>(fft, t); return true;
+    }
+    return false;
+}
+// Image of one transform: [lower-half tables | upper-half tables], each table
+// 24 dwords; logs[slot] are the reference's twiddle logs for that transform.
+void split_image(const Field &F, const SplitTabs &t, const uint32_t *logs, uint32_t *out) {
+    const size_t nt = t.lo.size();
+    for (size_t i = 0; i < nt; i++) {
+        make_twiddle(F, t.lo[i] < 0 ? F.mod : logs[t.lo[i]], out + i * kTwDwords16, true);
+        make_twiddle(F, t.hi[i] < 0 ? F.mod : logs[t.hi[i]], out + (nt + i) * kTwDwords16, true);
+    }
+}
+int upload_split(rs_codec *c) {
+    SplitTabs ti, tf;
+    if (!split_tabs(c->logm, false, ti) || !split_tabs(c->logm, true, tf)) return RS_OK;
+    const int is = ifft_slots(c->logm);
+    const size_t ni = 2 * ti.lo.size() * kTwDwords16, nf = 2 * tf.lo.size() * kTwDwords16;
+    std::vector<uint32_t> hi((size_t)c->nchunks * ni), hf(std::max<size_t>(nf, 1));
+    for (int ch = 0; ch < c->nchunks; ch++) split_image(*c->F, ti, c->enc_ifft_logs.data() + (size_t)ch * is, hi.data() + ch * ni);
+    split_image(*c->F, tf, c->enc_fft_logs.data(), hf.data());
+    HIP_TRY(c->tws_ifft.ensure(hi.size()));
+    HIP_TRY(c->tws_fft.ensure(hf.size()));
+    HIP_TRY(hipMemcpy(c->tws_ifft.p, hi.data(), hi.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->tws_fft.p, hf.data(), hf.size() * 4, hipMemcpyHostToDevice));
+    c->split_ok = true;
+    return RS_OK;
+}
+
+// RS_NO_SPLIT=1 disables the split kernel (A/B experiments only).
+bool split_enabled() {
+    const char *e = getenv("RS_NO_SPLIT");
+    return !(e && e[0] == '1');
+}
+
 // Host half of the encode plan (no device calls): twiddle schedule and panic check.
 void plan_encode_host(rs_codec *c) {
     c->enc_ok = encode_schedule(*c->F, c->k, c->p, c->enc_ifft_logs, c->enc_fft_logs, c->nchunks);
     c->path = !c->enc_ok ? "panic" : (c->logm <= kMaxRegLogM ? encode_reg_name(c->bits, c->logm) : "multipass");
+    if (c->enc_ok && c->bits == 16 && c->logm >= 2 && c->logm <= 5 && split_enabled())
+        c->path = std::string("split16-m") + std::to_string(c->m);
 }
 
 // Device half, on first use: stream, flag word, encode twiddle tables.
@@ -159,6 +219,10 @@ int ensure_device(rs_codec *c) {
         if (e) return e;
         e = upload_twiddles(c, c->enc_fft_logs, c->tw_fft);
         if (e) return e;
+        if (c->bits == 16 && split_enabled()) {
+            e = upload_split(c);
+            if (e) return e;
+        }
     }
     c->dev_ready = true;
     return RS_OK;
@@ -253,6 +317,14 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
         a.tw_ifft = c->tw_ifft.p;
         a.tw_fft = c->tw_fft.p;
         a.mismatch = mismatch;
+        // split kernel: strided rows whose data span fits a 32-bit buffer offset
+        const uint64_t span = (uint64_t)(c->k - 1) * data.stride + S;
+        if (c->split_ok && !data.table && !par.table && span < (1ull << 32)) {
+            a.tw_ifft = c->tws_ifft.p;
+            a.tw_fft = c->tws_fft.p;
+            HIP_TRY(launch_encode_split(c->logm, mismatch != nullptr, a, s));
+            return RS_OK;
+        }
         HIP_TRY(launch_encode_reg(c->bits, c->logm, mismatch != nullptr, a, s));
         return RS_OK;
     }
@@ -537,6 +609,156 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
 
 }  // namespace
 
+// Host simulation of the split schedules against the plain op lists on random
+// GF(2^16) symbols and random twiddle logs (modulus included): returns the
+// number of differing rows over both transforms (0 = identical).
+namespace {
+template <class OPS, class SCH>
+int split_sim_one(const Field &F, const SCH &s, uint32_t &seed) {
+    constexpr OPS ops{};
+    constexpr int M = SCH::M, HM = SCH::HM;
+    auto rnd = [&]() { seed = seed * 1664525u + 1013904223u; return seed >> 8; };
+    std::vector<uint32_t> logs(OPS::N + 1);
+    for (auto &l : logs) l = (rnd() % 5 == 0) ? F.mod : rnd() % F.mod;
+    std::vector<uint32_t> in(M), ref(M);
+    for (int r = 0; r < M; r++) in[r] = ref[r] = rnd() & 0xFFFF;
+    auto mul = [&](uint32_t v, uint32_t lg) -> uint32_t { return (v == 0 || lg == F.mod) ? 0 : F.mul_log(v, lg); };
+    for (int i = 0; i < OPS::N; i++) {
+        const BOp o = ops.op[i];
+        uint32_t &x = ref[o.x], &y = ref[o.y];
+        if (o.kind == OP_IFFT) { y ^= x; x ^= mul(y, logs[o.slot]); }
+        else if (o.kind == OP_FFT) { x ^= mul(y, logs[o.slot]); y ^= x; }
+        else y ^= x;
+    }
+    uint32_t reg[2][HM > 0 ? HM : 1];
+    for (int r = 0; r < M; r++) {
+        // initial layout: the schedule's row0 (lower) and its bit-h0 partner (upper)
+        for (int k = 0; k < HM; k++) {
+            if (s.row0[k] == r) reg[0][k] = in[r];
+            if ((s.row0[k] | (1 << s.h0)) == r) reg[1][k] = in[r];
+        }
+    }
+    for (int i = 0; i < s.nsteps; i++) {
+        const SStep st = s.step[i];
+        if (st.type == ST_SWAP) { std::swap(reg[1][st.a], reg[0][st.b]); continue; }
+        for (int h = 0; h < 2; h++) {
+            uint32_t &x = reg[h][st.a], &y = reg[h][st.b];
+            const int slot = st.tab < 0 ? -1 : (h ? s.tab_hi[st.tab] : s.tab_lo[st.tab]);
+            const uint32_t lg = slot < 0 ? F.mod : logs[slot];
+            if (st.kind == OP_IFFT) { y ^= x; x ^= mul(y, lg); }
+            else if (st.kind == OP_FFT) { x ^= mul(y, lg); y ^= x; }
+            else y ^= x;
+        }
+    }
+    int bad = 0;
+    for (int h = 0; h < 2; h++)
+        for (int k = 0; k < HM; k++) bad += reg[h][k] != ref[s.fin_row[h][k]];
+    return bad;
+}
+template <int L>
+int split_sim(const Field &F, uint32_t seed) {
+    int bad = 0;
+    for (int it = 0; it < 8; it++) {
+        bad += split_sim_one<IfftOps<L>>(F, EncodeSplit<L>::ifft, seed);
+        bad += split_sim_one<FftOps<L>>(F, EncodeSplit<L>::fft, seed);
+    }
+    // the chunk IFFT must end in the split bit the FFT starts from
+    if (EncodeSplit<L>::ifft.hend != EncodeSplit<L>::fft.h0) bad += 1000;
+    return bad;
+}
+}  // namespace
+
+// Host emulation of k_encode_split (data flow of the kernel, bit for bit):
+// twiddle images from split_image (as uploaded), the byte-permute multiply of
+// F16::mul_add, the half-wave swaps and the row layouts of schedule.hpp.
+namespace {
+inline uint32_t emu_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+    const uint64_t d = ((uint64_t)s0 << 32) | s1;
+    uint32_t r = 0;
+    for (int b = 0; b < 4; b++) r |= (uint32_t)((d >> (8 * ((sel >> (8 * b)) & 7))) & 0xFF) << (8 * b);
+    return r;
+}
+inline void emu_mul_add(uint32_t &xl, uint32_t &xh, uint32_t lo, uint32_t hi, const uint32_t *t) {
+    const uint32_t a0 = lo & 0x07070707u, a1 = (lo >> 3) & 0x07070707u, a2 = (lo >> 6) & 0x03030303u;
+    const uint32_t b0 = hi & 0x07070707u, b1 = (hi >> 3) & 0x07070707u, b2 = (hi >> 6) & 0x03030303u;
+    xl ^= emu_perm(t[1], t[0], a0) ^ emu_perm(t[5], t[4], a1) ^ emu_perm(t[8], t[8], a2) ^ emu_perm(t[11], t[10], b0) ^
+          emu_perm(t[15], t[14], b1) ^ emu_perm(t[18], t[18], b2);
+    xh ^= emu_perm(t[3], t[2], a0) ^ emu_perm(t[7], t[6], a1) ^ emu_perm(t[9], t[9], a2) ^ emu_perm(t[13], t[12], b0) ^
+          emu_perm(t[17], t[16], b1) ^ emu_perm(t[19], t[19], b2);
+}
+template <class SCH>
+void emu_run(const SCH &s, uint32_t (*rl)[16], uint32_t (*rh)[16], const uint32_t *img) {
+    const int nt = s.ntab;
+    for (int i = 0; i < s.nsteps; i++) {
+        const SStep st = s.step[i];
+        if (st.type == ST_SWAP) {
+            std::swap(rl[1][st.a], rl[0][st.b]);
+            std::swap(rh[1][st.a], rh[0][st.b]);
+            continue;
+        }
+        for (int h = 0; h < 2; h++) {
+            uint32_t &xl = rl[h][st.a], &xh = rh[h][st.a], &yl = rl[h][st.b], &yh = rh[h][st.b];
+            const uint32_t *t = st.tab >= 0 ? img + (size_t)(h * nt + st.tab) * kTwDwords16 : nullptr;
+            if (st.kind == OP_IFFT) {
+                yl ^= xl; yh ^= xh;
+                emu_mul_add(xl, xh, yl, yh, t);
+            } else if (st.kind == OP_FFT) {
+                emu_mul_add(xl, xh, yl, yh, t);
+                yl ^= xl; yh ^= xh;
+            } else {
+                yl ^= xl; yh ^= xh;
+            }
+        }
+    }
+}
+template <int L>
+int emu_split(rs_codec *c, const uint8_t *data, uint8_t *parity, uint64_t S) {
+    const auto &SI = EncodeSplit<L>::ifft;
+    const auto &SF = EncodeSplit<L>::fft;
+    constexpr int M = 1 << L, HM = M / 2;
+    SplitTabs ti, tf;
+    split_tabs(L, false, ti);
+    split_tabs(L, true, tf);
+    const int is = ifft_slots(L);
+    const size_t ni = 2 * ti.lo.size() * kTwDwords16;
+    std::vector<uint32_t> imi((size_t)c->nchunks * ni), imf(2 * tf.lo.size() * kTwDwords16 + 1);
+    for (int ch = 0; ch < c->nchunks; ch++) split_image(*c->F, ti, c->enc_ifft_logs.data() + (size_t)ch * is, imi.data() + ch * ni);
+    split_image(*c->F, tf, c->enc_fft_logs.data(), imf.data());
+    auto dword = [&](const uint8_t *row, uint64_t off) { uint32_t v; std::memcpy(&v, row + off, 4); return v; };
+    for (uint64_t u = 0; u < S / 8; u++) {
+        const uint64_t lo_off = (u / 8) * 64 + (u % 8) * 4;
+        uint32_t al[2][16] = {}, ah[2][16] = {};
+        for (int ch = 0; ch < c->nchunks; ch++) {
+            uint32_t cl[2][16] = {}, chh[2][16] = {};
+            for (int h = 0; h < 2; h++)
+                for (int k = 0; k < HM; k++) {
+                    const int row = ch * M + SI.row0[k] + h * (1 << SI.h0);
+                    if (row < c->k) {
+                        cl[h][k] = dword(data + (size_t)row * S, lo_off);
+                        chh[h][k] = dword(data + (size_t)row * S, lo_off + 32);
+                    }
+                }
+            emu_run(SI, cl, chh, imi.data() + ch * ni);
+            for (int h = 0; h < 2; h++)
+                for (int k = 0; k < HM; k++) {
+                    al[h][k] ^= cl[h][k];
+                    ah[h][k] ^= chh[h][k];
+                }
+        }
+        emu_run(SF, al, ah, imf.data());
+        for (int h = 0; h < 2; h++)
+            for (int k = 0; k < HM; k++) {
+                const int row = SF.fin_row[h][k];
+                if (row < c->p) {
+                    std::memcpy(parity + (size_t)row * S + lo_off, &al[h][k], 4);
+                    std::memcpy(parity + (size_t)row * S + lo_off + 32, &ah[h][k], 4);
+                }
+            }
+    }
+    return RS_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int rs_new(int field_bits, int data_shards, int parity_shards, int device, rs_codec **out) {
@@ -781,6 +1003,28 @@ int rs_debug_error_locators(int bits, int k, int p, const uint8_t *erased, uint3
     if (!error_locators(field(bits), k, p, erased, el)) return RS_ERR_PANIC;
     std::copy(el.begin(), el.end(), out);
     return RS_OK;
+}
+
+int rs_debug_split_emulate(rs_codec *c, const uint8_t *data, uint8_t *parity, size_t S) {
+    if (!c || !data || !parity || S % 64 || c->bits != 16 || !c->enc_ok) return RS_ERR_INVALID_ARG;
+    switch (c->logm) {
+        case 2: return emu_split<2>(c, data, parity, S);
+        case 3: return emu_split<3>(c, data, parity, S);
+        case 4: return emu_split<4>(c, data, parity, S);
+        case 5: return emu_split<5>(c, data, parity, S);
+    }
+    return RS_ERR_INVALID_ARG;
+}
+
+int rs_debug_split_check(int logm, uint32_t seed) {
+    const Field &F = field(16);
+    switch (logm) {
+        case 2: return split_sim<2>(F, seed);
+        case 3: return split_sim<3>(F, seed);
+        case 4: return split_sim<4>(F, seed);
+        case 5: return split_sim<5>(F, seed);
+    }
+    return -1;
 }
 
 const char *rs_strerror(int code) {

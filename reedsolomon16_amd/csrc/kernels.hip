@@ -17,6 +17,7 @@
 //   IFFT: y ^= x; x ^= y*m        FFT: x ^= y*m; y ^= x
 //   log_m == modulus means a zero twiddle: XOR only (wave-uniform branch).
 #include "kernels.hpp"
+#include "schedule.hpp"
 
 // Performance-experiment knobs (scripts/ablate.sh builds separate libraries
 // with these; the product build defines none of them):
@@ -51,6 +52,12 @@ __device__ unsigned long long g_rs_stamps[3 << 16];
 // RS_OP_PIN: chain every butterfly op's outputs with an empty asm (bounds code motion).
 #ifndef RS_ABL_IFFT_AS_FFT
 #define RS_ABL_IFFT_AS_FFT 0  // timing experiment only: run the FFT op list per chunk (wrong result)
+#endif
+#ifndef RS_SPLIT_PREQ
+#define RS_SPLIT_PREQ 3  // quads (of 5) of the next twiddle table prefetched by the split kernel
+#endif
+#ifndef RS_SPLIT_PIN
+#define RS_SPLIT_PIN 1
 #endif
 #ifndef RS_DMA_SPREAD
 #define RS_DMA_SPREAD 1
@@ -320,67 +327,8 @@ __device__ __forceinline__ uint8_t *row_ptr(const RowSet &rs, int i) {
 }
 
 // ---------------------------------------------------------------- register transforms (M <= 32)
-// A transform is a compile-time list of radix-2 butterfly ops over the M
-// registers.  Kinds: IFFT (y ^= x; x ^= y*t), FFT (x ^= y*t; y ^= x) and
-// FFT-XOR (y ^= x, zero twiddle).  Orders and twiddle slots follow
-//   ifftDITEncoder leopard16.go:694-741: radix-4 pairs at dist 1,4,16 (m01 on
-//     (i,i+d), m23 on (i+2d,i+3d), then m02 on (i,i+2d),(i+d,i+3d)), and a
-//     radix-2 layer at M/2 when log2(M) is odd;
-//   fftDIT leopard16.go:618-657: radix-4 pairs at dist M/4, M/16, ... (m02
-//     first, then m01 / m23), and a radix-2 layer at dist 1 when log2(M) is odd.
-// The reference skips IFFT groups with r >= mtrunc: those rows are zero here,
-// and any twiddle maps zero rows to zero rows, so computing them is equivalent.
-// In the FFT, the r = 0 group's m01 = fftSkew[dist-1] and m02 = fftSkew[2*dist-1]
-// (and the radix-2 fftSkew[0]) are fftSkew[2^j - 1] = log(0) (initFFTSkew
-// leopard16.go:997), so they are XOR-only by construction (checked on the host
-// in encode_schedule).  FFT rows >= p are computed but never stored.
-enum : int { OP_IFFT = 0, OP_FFT = 1, OP_FFTX = 2 };
-struct BOp {
-    int x, y, slot, kind;
-};
-// Within a radix-4 group the ops are ordered by twiddle (all m01 butterflies,
-// then all m23, then all m02 for the IFFT; m02, m01, m23 for the FFT) so
-// consecutive ops share a table; this is legal because butterflies of one
-// layer over different i are independent.
-template <int LOGM>
-struct IfftOps {
-    static constexpr int M = 1 << LOGM, N = (M / 2) * LOGM;
-    BOp op[N > 0 ? N : 1];
-    constexpr IfftOps() : op() {
-        int n = 0, slot = 0, dist = 1;
-        for (; dist * 4 <= M; dist *= 4)
-            for (int r = 0; r < M; r += 4 * dist, slot += 3) {
-                for (int i = r; i < r + dist; i++) op[n++] = BOp{i, i + dist, slot, OP_IFFT};                   // m01
-                for (int i = r; i < r + dist; i++) op[n++] = BOp{i + 2 * dist, i + 3 * dist, slot + 2, OP_IFFT};  // m23
-                for (int i = r; i < r + dist; i++) {                                                             // m02
-                    op[n++] = BOp{i, i + 2 * dist, slot + 1, OP_IFFT};
-                    op[n++] = BOp{i + dist, i + 3 * dist, slot + 1, OP_IFFT};
-                }
-            }
-        if (dist < M)
-            for (int i = 0; i < M / 2; i++) op[n++] = BOp{i, i + M / 2, slot, OP_IFFT};
-    }
-};
-template <int LOGM>
-struct FftOps {
-    static constexpr int M = 1 << LOGM, N = (M / 2) * LOGM;
-    BOp op[N > 0 ? N : 1];
-    constexpr FftOps() : op() {
-        int n = 0, slot = 0, dist = M / 4;
-        for (; dist != 0; dist /= 4)
-            for (int r = 0; r < M; r += 4 * dist, slot += 3) {
-                const int k0 = r == 0 ? OP_FFTX : OP_FFT;
-                for (int i = r; i < r + dist; i++) {  // m02
-                    op[n++] = BOp{i, i + 2 * dist, slot + 1, k0};
-                    op[n++] = BOp{i + dist, i + 3 * dist, slot + 1, k0};
-                }
-                for (int i = r; i < r + dist; i++) op[n++] = BOp{i, i + dist, slot, k0};                          // m01
-                for (int i = r; i < r + dist; i++) op[n++] = BOp{i + 2 * dist, i + 3 * dist, slot + 2, OP_FFT};  // m23
-            }
-        if (LOGM & 1)
-            for (int r = 0; r < M; r += 2) op[n++] = BOp{r, r + 1, slot + r / 2, r == 0 ? OP_FFTX : OP_FFT};
-    }
-};
+// Op lists (IfftOps / FftOps) and the half-wave split schedules live in
+// schedule.hpp, shared with the host.
 
 // Twiddle table held in registers (wave-uniform -> SGPRs).
 template <class F>
@@ -405,6 +353,19 @@ __device__ __forceinline__ Tab<F> lds_tab(uint32_t vaddr, int byte_off) {
             if (4 * q + j < F::TWU) r.v[4 * q + j] = x[j];
     }
     return r;
+}
+
+// Quads [qb, qe) of a table (16 bytes each) into r.
+template <class F>
+__device__ __forceinline__ void lds_tab_part(Tab<F> &r, uint32_t vaddr, int byte_off, int qb, int qe) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int q = qb; q < qe; q++) {
+        const u32x4 x = *(const volatile __attribute__((address_space(3))) u32x4 *)(uintptr_t)(vaddr + byte_off + 16 * q);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (4 * q + j < F::TWU) r.v[4 * q + j] = x[j];
+    }
 }
 
 // Loaded through the constant address space: read-only for the whole launch,
@@ -517,7 +478,8 @@ constexpr int fft_slot_count(int logm) {
     return s;
 }
 
-// 32-bit LDS address of p, materialized in a VGPR (opaque to the compiler) so
+// 32-bit LDS address of p (wave-uniform: it passes through an SGPR),
+// materialized in a VGPR (opaque to the compiler) so
 // that constant offsets from it use the DS instruction's offset field instead
 // of one SGPR add + v_mov per access.
 __device__ __forceinline__ uint32_t vgpr_lds_addr(const uint8_t *p) {
@@ -728,6 +690,255 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- half-wave split encode (GF(2^16), 4 <= m <= 32)
+// Same algorithm as k_encode_reg, but the M rows of a column unit are split
+// over lanes L and L+32 (schedule.hpp, SplitSched): per lane M/2 rows of the
+// chunk and of the accumulator, so the kernel fits 128 VGPRs and runs 4 waves
+// per SIMD (k_encode_reg needs ~240 VGPRs at m = 32: 2 waves per SIMD, and
+// its twiddle-table reads stay exposed).  A wave covers 32 column units
+// (256 bytes of every row).  Each half-wave reads its own twiddle table: the
+// host lays out each transform's table loads as [lower half | upper half].
+// Rows are staged HBM -> LDS by MUBUF LDS-DMA (next chunk during this one).
+template <int L>
+struct IfftSplit {
+    static constexpr auto s = EncodeSplit<L>::ifft;
+};
+template <int L>
+struct FftSplit {
+    static constexpr auto s = EncodeSplit<L>::fft;
+};
+
+template <class SRC>
+__device__ __forceinline__ void run_split(F16<1>::Vec *w, uint32_t ltab) {
+    typedef F16<1> F;
+    constexpr auto sch = SRC::s;
+    constexpr int NS = sch.nsteps;
+    constexpr int NT = sch.ntab;
+    constexpr int TB = F::TWD * 4;
+    constexpr int NQ = (F::TWU + 3) / 4;              // quads per table
+    constexpr int PQ = RS_SPLIT_PREQ < NQ ? RS_SPLIT_PREQ : NQ;  // quads of the next table prefetched
+    Tab<F> t0, t1;
+    if constexpr (NT > 0) lds_tab_part<F>(t0, ltab, 0, 0, NQ);
+    int have = 0;
+#pragma unroll
+    for (int i = 0; i < NS; i++) {
+        const SStep st = sch.step[i];
+        if (st.type == ST_SWAP) {
+            const auto rl = __builtin_amdgcn_permlane32_swap(w[st.a].l[0], w[st.b].l[0], false, false);
+            const auto rh = __builtin_amdgcn_permlane32_swap(w[st.a].h[0], w[st.b].h[0], false, false);
+            w[st.a].l[0] = rl[0];
+            w[st.b].l[0] = rl[1];
+            w[st.a].h[0] = rh[0];
+            w[st.b].h[0] = rh[1];
+            continue;
+        }
+        const int need = RS_ABL_TAB_ONCE ? (st.tab >= 0 ? 0 : -1) : st.tab;
+        if (need >= 0 && need != have) {  // next table run: its first PQ quads were prefetched into t1
+#pragma unroll
+            for (int j = 0; j < 4 * PQ && j < F::TWU; j++) t0.v[j] = t1.v[j];
+            lds_tab_part<F>(t0, ltab, need * TB, PQ, NQ);
+            have = need;
+        }
+        bool first = need >= 0;
+        if (first) {
+            for (int j = 0; j < i; j++)
+                if (sch.step[j].type == ST_OP && sch.step[j].tab == need) first = false;
+        }
+        if (first) {
+            if (have + 1 < NT) lds_tab_part<F>(t1, ltab, (have + 1) * TB, 0, PQ);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        typename F::Vec &x = w[st.a], &y = w[st.b];
+        if (st.kind == OP_IFFT) {
+            F::xor_into(y, x);
+            F::mul_add(x, y, t0.v);
+        } else if (st.kind == OP_FFT) {
+            F::mul_add(x, y, t0.v);
+            F::xor_into(y, x);
+        } else {
+            F::xor_into(y, x);
+        }
+#if RS_SPLIT_PIN
+        F::pin(x);
+        F::pin(y);
+#endif
+    }
+}
+
+template <int LOGM>
+struct SplitGeom {
+    typedef EncodeSplit<LOGM> ES;
+    static constexpr int M = 1 << LOGM, HM = M / 2;
+    static constexpr int ROWB = 256;                 // bytes of a row per wave (32 units x 8 B)
+    static constexpr int NDMA = M * ROWB / 1024;     // LDS-DMA wave-instructions per chunk
+    static constexpr int TB = F16<1>::TWD * 4;
+    static constexpr int NTI = ES::ifft.ntab, NTF = ES::fft.ntab;
+    static constexpr int TABB = 2 * (NTI > NTF ? NTI : NTF) * TB;  // one table buffer
+    static constexpr int LDS = 4 * M * ROWB + 2 * TABB;
+};
+
+template <int LOGM, bool VERIFY>
+__global__ void __launch_bounds__(256, 4) k_encode_split(EncodeArgs a) {
+    typedef F16<1> F;
+    typedef typename F::Vec V;
+    typedef SplitGeom<LOGM> G;
+    typedef typename G::ES ES;
+    constexpr int M = G::M, HM = G::HM, ROWB = G::ROWB, NDMA = G::NDMA, TB = G::TB;
+    constexpr int NTI = G::NTI, NTF = G::NTF, TABB = G::TABB;
+    constexpr auto SI = ES::ifft;
+    constexpr auto SF = ES::fft;
+    constexpr int H0 = SI.h0, HF = SF.hend;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint8_t lds[G::LDS];
+    uint8_t *ltab = lds + 4 * M * ROWB;
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int cu = lane & 31, half = lane >> 5;
+    const uint64_t units = a.shard_size >> 3;  // 8-byte column units (4 symbols)
+    const uint64_t u0 = ((uint64_t)blockIdx.x * 4 + wave) * 32;
+    const bool wave_live = u0 < units;
+    const bool lane_live = u0 + cu < units;
+    const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
+    const uint32_t span = (uint32_t)(u0 * 8);                      // wave's byte offset in a row
+    const uint32_t colb = (cu >> 3) * 64 + (cu & 7) * 4;           // lane's lo dword within the wave's 256 B
+    uint8_t *img = lds + wave * (M * ROWB);
+
+    const __amdgpu_buffer_rsrc_t drsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.data.base + soff), 0, (int)(uint32_t)((uint64_t)(a.k - 1) * a.data.stride + a.shard_size), 0x00020000);
+    // chunk c's rows: piece P = 16 bytes; row P / 16, piece P % 16 of the wave's 256 B.
+    // Full chunks of full-width waves: per-lane offset fixed, row base in soffset
+    // (no per-lane predicates to keep live across the loop).
+    const bool wave_full = (uint64_t)span + ROWB <= a.shard_size;
+    const uint32_t lane_off = (uint32_t)((lane >> 4) * a.data.stride) + (lane & 15) * 16 + span;
+    auto stage_one = [&](int c, int j) {
+        const int row0 = c * M, cnt = a.k - row0;
+        if (wave_full && cnt >= M) {
+            const uint32_t so = (uint32_t)((uint64_t)(row0 + 4 * j) * a.data.stride);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(drsrc, (lvoid_t *)(img + j * 1024), 16, lane_off, so, 0, 0);
+            return;
+        }
+        const int P = j * 64 + lane;
+        const int r = P >> 4;
+        const uint32_t go = span + (P & 15) * 16;
+        if (wave_live && r < cnt && go < a.shard_size) {
+            const uint32_t voff = (uint32_t)((uint64_t)(row0 + r) * a.data.stride + go);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(drsrc, (lvoid_t *)(img + j * 1024), 16, voff, 0, 0, 0);
+        } else {
+            *(__attribute__((address_space(3))) u32x4 *)(img + j * 1024 + lane * 16) = u32x4{0, 0, 0, 0};
+        }
+    };
+    auto stage_tab = [&](const uint32_t *src, int nbytes, int b) {
+        const int npieces = nbytes / 16;
+        const int P = wave * 64 + lane;
+        const __amdgpu_buffer_rsrc_t trsrc = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, nbytes, 0x00020000);
+        for (int base = 0; base < npieces; base += 256)
+            if (base + P < npieces)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(trsrc, (lvoid_t *)(ltab + b * TABB + base * 16 + wave * 1024),
+                                                         16, (base + P) * 16, 0, 0, 0);
+    };
+    constexpr int IMGB = 2 * NTI * TB, FMGB = 2 * NTF * TB;  // bytes of one chunk's / the FFT's table image
+
+#if RS_STAMP
+    const unsigned long long st_c0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long st_first = 0, st_wait = 0;
+    const unsigned swave = blockIdx.x * 4 + wave;
+#endif
+    V acc[HM];
+#pragma unroll
+    for (int j = 0; j < NDMA; j++) stage_one(0, j);
+    stage_tab(a.tw_ifft, IMGB, 0);
+    // lane's LDS read base: register k holds row row0[k] (lower) / row0[k] | 1 << H0 (upper)
+    const uint8_t *rd = img + half * ((1 << H0) * ROWB) + colb;
+    for (int c = 0; c < a.nchunks; ++c) {
+#if RS_STAMP
+        const unsigned long long sw0 = __builtin_amdgcn_s_memtime();
+#endif
+        wait_vm0();
+        __syncthreads();
+#if RS_STAMP
+        {
+            const unsigned long long sw1 = __builtin_amdgcn_s_memtime();
+            if (c == 0) st_first = sw1 - st_c0;
+            else st_wait += sw1 - sw0;
+        }
+#endif
+        V cur[HM];
+#pragma unroll
+        for (int k = 0; k < HM; k++) {
+            const uint8_t *p = rd + SI.row0[k] * ROWB;
+            cur[k].l[0] = *(const __attribute__((address_space(3))) uint32_t *)p;
+            cur[k].h[0] = *(const __attribute__((address_space(3))) uint32_t *)(p + 32);
+        }
+        wait_lgkm0();  // reads done before the image is overwritten
+        const bool more = c + 1 < a.nchunks;
+        if (more) stage_tab(a.tw_ifft + (uint64_t)(c + 1) * (IMGB / 4), IMGB, (c + 1) & 1);
+        else stage_tab(a.tw_fft, FMGB, (c + 1) & 1);
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < NDMA; j++) stage_one(c + 1, j);
+        }
+        run_split<IfftSplit<LOGM>>(cur, vgpr_lds_addr(ltab + (c & 1) * TABB) + (uint32_t)half * (NTI * TB));
+        if (c == 0) {
+#pragma unroll
+            for (int k = 0; k < HM; k++) acc[k] = cur[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < HM; k++) F::xor_into(acc[k], cur[k]);
+        }
+#if RS_STAMP
+        if (lane == 0 && blockIdx.y == 0 && c < 8 && swave < 8192) {
+            g_rs_stamps[65536 + 16 * swave + 2 * c] = __builtin_amdgcn_s_memtime() - sw0;
+            g_rs_stamps[65536 + 16 * swave + 2 * c + 1] = sw0 - st_c0;
+        }
+#endif
+    }
+#if RS_STAMP
+    const unsigned long long sf0 = __builtin_amdgcn_s_memtime();
+#endif
+    wait_vm0();
+    __syncthreads();
+#if RS_STAMP
+    const unsigned long long sf1 = __builtin_amdgcn_s_memtime();
+#endif
+    run_split<FftSplit<LOGM>>(acc, vgpr_lds_addr(ltab + (a.nchunks & 1) * TABB) + (uint32_t)half * (NTF * TB));
+#if RS_STAMP
+    if (lane == 0 && blockIdx.y == 0 && swave < 8192) {
+        const unsigned long long sf2 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        g_rs_stamps[32768 + 4 * swave] = st_first;
+        g_rs_stamps[32768 + 4 * swave + 1] = st_wait + (sf1 - sf0);
+        g_rs_stamps[32768 + 4 * swave + 2] = sf2 - sf1;
+        g_rs_stamps[32768 + 4 * swave + 3] = sf0 - st_c0;
+        g_rs_stamps[4 * swave] = sf2 - st_c0;
+        g_rs_stamps[4 * swave + 1] = r1 - st_r0;
+        g_rs_stamps[4 * swave + 2] = st_r0;
+        g_rs_stamps[4 * swave + 3] = 0;
+    }
+#endif
+    if (!lane_live) return;
+    // register k, half h holds parity row fin_row[h][k]; the two halves' rows differ by 1 << HF
+    const uint64_t prow_step = (uint64_t)a.parity.stride;
+    uint8_t *pbase = a.parity.base + soff + span + colb + (uint64_t)half * ((uint64_t)(1 << HF) * prow_step);
+    uint32_t bad = 0;
+#pragma unroll
+    for (int k = 0; k < HM; k++) {
+        const int row = SF.fin_row[0][k] + half * (1 << HF);
+        if (row < a.p) {
+            uint8_t *q = pbase + (uint64_t)SF.fin_row[0][k] * prow_step;
+            if constexpr (VERIFY) {
+                bad |= (*(const __attribute__((address_space(1))) uint32_t *)q ^ acc[k].l[0]) |
+                       (*(const __attribute__((address_space(1))) uint32_t *)(q + 32) ^ acc[k].h[0]);
+            } else {
+                *(__attribute__((address_space(1))) uint32_t *)q = acc[k].l[0];
+                *(__attribute__((address_space(1))) uint32_t *)(q + 32) = acc[k].h[0];
+            }
+        }
+    }
+    if constexpr (VERIFY) {
+        if (bad) atomicOr(a.mismatch, 1);
+    }
+}
+
 // ---------------------------------------------------------------- multi-pass kernels (any m / n)
 // Each thread owns one column unit of one butterfly; rows live in a
 // contiguous work slab (row stride = S).  Used for m > 32 and for decode.
@@ -889,6 +1100,15 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 
 // Lane width per (field, log2 m): keep acc + work + prefetch <= ~192 VGPRs
 // (2 waves/SIMD) while using the widest coalesced access that fits.
+template <int LOGM>
+hipError_t launch_split_t(bool verify, const EncodeArgs &a, hipStream_t s) {
+    const uint64_t units = a.shard_size >> 3;
+    dim3 grid((unsigned)((units + 127) / 128), (unsigned)a.nstripes);
+    if (verify) hipLaunchKernelGGL((k_encode_split<LOGM, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_encode_split<LOGM, false>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_encode_reg(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
     if (bits == 16) {
         switch (logm) {
@@ -908,6 +1128,16 @@ hipError_t launch_encode_reg(int bits, int logm, bool verify, const EncodeArgs &
             case 4: return enc_reg<F8<4>, 4>(verify, a, s);
             case 5: return enc_reg<F8<2>, 5>(verify, a, s);
         }
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_encode_split(int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
+    switch (logm) {
+        case 2: return launch_split_t<2>(verify, a, s);
+        case 3: return launch_split_t<3>(verify, a, s);
+        case 4: return launch_split_t<4>(verify, a, s);
+        case 5: return launch_split_t<5>(verify, a, s);
     }
     return hipErrorInvalidValue;
 }

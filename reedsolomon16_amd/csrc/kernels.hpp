@@ -32,6 +32,12 @@ struct EncodeArgs {
 
 // Returns hipSuccess or the launch error.  logm in [0, 5].
 hipError_t launch_encode_reg(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
+// Half-wave split encode (GF(2^16), logm 2..5, strided rows only: data.table ==
+// nullptr, and (k-1)*stride + shard_size < 2^32).  tw_ifft = nchunks images of
+// split_image_dwords(logm, false) dwords, tw_fft = one image of
+// split_image_dwords(logm, true) dwords (codec.cpp lays them out from
+// schedule.hpp's EncodeSplit<logm>).
+hipError_t launch_encode_split(int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 // Name of the register-kernel variant (for diagnostics / profiles).
 const char *encode_reg_name(int bits, int logm);
 

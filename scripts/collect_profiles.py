@@ -24,6 +24,9 @@ def short(name: str) -> str:
 
 def path_of(name: str):
     """k_encode_reg<F16<W>, LOGM, VERIFY, TABLE> -> the engine's path name (codec.cpp)."""
+    m = re.search(r"k_encode_split<(\d+), (false|true)>", name)
+    if m:
+        return f"split16-m{1 << int(m.group(1))}" + ("-verify" if m.group(2) == "true" else "")
     m = re.search(r"k_encode_reg<rs::\(anonymous namespace\)::F(16|8)<\d+>, (\d+), (false|true)", name)
     if not m:
         return None

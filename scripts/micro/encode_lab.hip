@@ -29,10 +29,11 @@ int main(int argc, char **argv) {
     (void)hipEventElapsedTime(&ms, e0, e1);
     std::vector<unsigned long long> st(3 << 16);
     (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_rs_stamps), st.size() * 8);
+    const int NW = getenv("RS_NO_SPLIT") ? 2048 : 4096;  // waves of the C3 launch
     double cyc = 0, rt = 0;
     int n = 0;
     unsigned long long t0 = ~0ull, t1 = 0;
-    for (int w = 0; w < 2048; w++) {
+    for (int w = 0; w < NW; w++) {
         if (st[4 * w + 1] == 0) continue;
         cyc += st[4 * w];
         rt += st[4 * w + 1];
@@ -44,7 +45,7 @@ int main(int argc, char **argv) {
     rt /= n;
     // histogram of wave start times (us after the first start) and per-CU residency
     int hist[16] = {0};
-    for (int w = 0; w < 2048; w++) {
+    for (int w = 0; w < NW; w++) {
         double s0 = (st[4 * w + 2] - t0) / 100.0;
         int b = (int)(s0 / 5.0);
         hist[b < 15 ? b : 15]++;
@@ -53,19 +54,19 @@ int main(int argc, char **argv) {
     for (int i = 0; i < 16; i++) printf(" %d", hist[i]);
     printf("\n");
     double f = 0, wt = 0, fft = 0, pre = 0;
-    for (int w = 0; w < 2048; w++) {
+    for (int w = 0; w < NW; w++) {
         f += st[32768 + 4 * w]; wt += st[32768 + 4 * w + 1]; fft += st[32768 + 4 * w + 2]; pre += st[32768 + 4 * w + 3];
     }
     printf("per wave (cycles): first-data wait %.0f | later chunk waits %.0f | IFFT phase total %.0f | FFT %.0f | after FFT %.0f\n",
-           f / 2048, wt / 2048, pre / 2048 - f / 2048 - wt / 2048, fft / 2048, cyc - pre / 2048 - fft / 2048);
+           f / NW, wt / NW, pre / NW - f / NW - wt / NW, fft / NW, cyc - pre / NW - fft / NW);
     double ch[8] = {0}, cs[8] = {0};
-    for (int w = 0; w < 2048; w++)
+    for (int w = 0; w < NW; w++)
         for (int c = 0; c < 4; c++) {
             ch[c] += st[65536 + 16 * w + 2 * c];
             cs[c] += st[65536 + 16 * w + 2 * c + 1];
         }
     printf("per chunk (cycles, incl. its top wait): ");
-    for (int c = 0; c < 4; c++) printf(" c%d start %.0f dur %.0f |", c, cs[c] / 2048, ch[c] / 2048);
+    for (int c = 0; c < 4; c++) printf(" c%d start %.0f dur %.0f |", c, cs[c] / NW, ch[c] / NW);
     printf("\n");
     unsigned long long hw0 = st[3];
     printf("sample hw_id/xcc of wave0: xcc=%llu hwid=0x%llx\n", hw0 >> 32, hw0 & 0xffffffffull);

@@ -128,7 +128,8 @@ def test_constructor_errors():
     c = rs.New(10, 4)
     assert c.field_bits == 8 and c.total_shards() == 14 and c.shard_size_multiple() == 64
     assert rs.New(200, 100).field_bits == 16
-    assert rs.New16(128, 32).encode_path == "reg16-m32"
+    assert rs.New16(128, 32).encode_path == "split16-m32"
+    assert rs.New16(10, 1).encode_path == "reg16-m1"
     assert rs.New16(1024, 256).encode_path == "multipass"
 
 
@@ -188,3 +189,26 @@ def test_split_join_mirror_reference():
         c.join(io.BytesIO(), shards, 4 * 256 + 1)
     with pytest.raises(rs.ErrTooFewShards):
         c.join(io.BytesIO(), shards[:3], 10)
+
+
+@pytest.mark.parametrize("logm", [2, 3, 4, 5])
+def test_split_schedule_equals_plain_transform(logm):
+    """The split kernel's compile-time schedules (schedule.hpp) compute the
+    same IFFT / FFT as the reference butterfly order, simulated on the host."""
+    for seed in (1, 2, 3):
+        assert rs.lib().rs_debug_split_check(logm, seed) == 0
+    assert rs.lib().rs_debug_split_check(6, 1) == -1
+
+
+@pytest.mark.parametrize("k,p,S", [(10, 4, 1024), (10, 6, 128), (3, 7, 64), (37, 9, 64), (33, 17, 128), (128, 32, 256),
+                                   (130, 32, 64)])
+def test_split_kernel_emulation_matches_oracle(k, p, S):
+    """Bit-level host emulation of the split kernel (images, v_perm multiply,
+    half-wave swaps) against the oracle."""
+    rng = np.random.default_rng(k * 31 + p)
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    ref = orc.encode(16, k, p, data)
+    c = rs.New16(k, p)
+    out = np.zeros((p, S), np.uint8)
+    assert rs.lib().rs_debug_split_emulate(c._h, data.ctypes.data, out.ctypes.data, S) == 0
+    assert np.array_equal(out, ref)
