@@ -117,9 +117,16 @@ def _host_rows(shards: Sequence):
 
 
 def _dev_rows(rows, total: int):
-    """torch CUDA tensors -> (ptr array, shard size)."""
+    """torch CUDA tensors -> (ptr array, shard size).  A 2-D [total, S] tensor
+    (rows contiguous) is turned into row pointers arithmetically: no per-row
+    tensor objects on the host path."""
     if hasattr(rows, "dim") and rows.dim() == 2:
-        rows = [rows[i] for i in range(rows.shape[0])]
+        if rows.shape[0] != total:
+            raise ErrTooFewShards("need %d shards, got %d" % (total, rows.shape[0]))
+        if not rows.is_cuda or rows.dtype.itemsize != 1 or rows.stride(1) != 1:
+            raise TypeError("device shards must be a uint8 CUDA tensor with contiguous rows")
+        base, stride = rows.data_ptr(), rows.stride(0)
+        return (C.c_void_p * total)(*range(base, base + total * stride, stride)), rows.shape[1]
     if len(rows) != total:
         raise ErrTooFewShards("need %d shards, got %d" % (total, len(rows)))
     ptrs = (C.c_void_p * total)()

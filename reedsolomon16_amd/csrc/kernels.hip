@@ -113,6 +113,10 @@ __device__ __forceinline__ void ldw_lds(const uint8_t *p, uint32_t (&v)[W]) {
     }
 }
 
+// Verify's mismatch word lives in host-mapped pinned memory (codec.cpp): every
+// writer stores the same 1, so a plain system-scope store suffices.
+__device__ __forceinline__ void flag_mismatch(int *f) { __hip_atomic_store(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
     return __builtin_amdgcn_perm(s0, s1, sel);
 }
@@ -682,7 +686,7 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
 #pragma unroll
         for (int r = 0; r < M; r++)
             if (r < a.p) bad |= F::diff(acc[r], F::load(rowp<TABLE>(a.parity, r, soff), u));
-        if (bad) atomicOr(a.mismatch, 1);
+        if (bad) flag_mismatch(a.mismatch);
     } else {
 #pragma unroll
         for (int r = 0; r < M; r++)
@@ -912,7 +916,10 @@ __global__ void __launch_bounds__(256, 4) k_encode_split(EncodeArgs a) {
         g_rs_stamps[4 * swave] = sf2 - st_c0;
         g_rs_stamps[4 * swave + 1] = r1 - st_r0;
         g_rs_stamps[4 * swave + 2] = st_r0;
-        g_rs_stamps[4 * swave + 3] = 0;
+        unsigned xcc, hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        g_rs_stamps[4 * swave + 3] = ((unsigned long long)xcc << 32) | hw;
     }
 #endif
     if (!lane_live) return;
@@ -935,7 +942,7 @@ __global__ void __launch_bounds__(256, 4) k_encode_split(EncodeArgs a) {
         }
     }
     if constexpr (VERIFY) {
-        if (bad) atomicOr(a.mismatch, 1);
+        if (bad) flag_mismatch(a.mismatch);
     }
 }
 
@@ -1019,7 +1026,7 @@ __global__ void __launch_bounds__(256) k_copy_out(RowSet out, const uint8_t *wor
     const int r = blockIdx.y + r_off;
     Bytes16::Vec v = Bytes16::load(work + (uint64_t)r * S, u);
     if constexpr (VERIFY) {
-        if (Bytes16::diff(v, Bytes16::load(row_ptr(out, r), u))) atomicOr(mismatch, 1);
+        if (Bytes16::diff(v, Bytes16::load(row_ptr(out, r), u))) flag_mismatch(mismatch);
     } else {
         Bytes16::store(row_ptr(out, r), u, v);
     }

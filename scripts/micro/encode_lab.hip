@@ -68,6 +68,25 @@ int main(int argc, char **argv) {
     printf("per chunk (cycles, incl. its top wait): ");
     for (int c = 0; c < 4; c++) printf(" c%d start %.0f dur %.0f |", c, cs[c] / NW, ch[c] / NW);
     printf("\n");
+    {   // end-time histogram (5 us bins) and per-XCD mean wave life / last end
+        int eh[20] = {0};
+        double xl[8] = {0}, xe[8] = {0};
+        int xn[8] = {0};
+        for (int w = 0; w < NW; w++) {
+            const double e = (st[4 * w + 2] + st[4 * w + 1] - t0) / 100.0;
+            int b = (int)(e / 5.0);
+            eh[b < 19 ? b : 19]++;
+            const int x = (int)((st[4 * w + 3] >> 32) & 7);
+            xl[x] += st[4 * w + 1] / 100.0;
+            xn[x]++;
+            if (e > xe[x]) xe[x] = e;
+        }
+        printf("wave end histogram (5 us bins):");
+        for (int i = 0; i < 20; i++) printf(" %d", eh[i]);
+        printf("\nper XCD: ");
+        for (int x = 0; x < 8; x++) printf(" [%d] n=%d life %.1f last %.1f |", x, xn[x], xn[x] ? xl[x] / xn[x] : 0.0, xe[x]);
+        printf("\n");
+    }
     unsigned long long hw0 = st[3];
     printf("sample hw_id/xcc of wave0: xcc=%llu hwid=0x%llx\n", hw0 >> 32, hw0 & 0xffffffffull);
     printf("kernel %.2f us/launch; waves %d; mean wave life %.0f shader cycles = %.2f us; clock %.3f GHz\n",
