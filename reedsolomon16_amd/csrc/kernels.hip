@@ -724,6 +724,8 @@ __device__ __forceinline__ void run_split(F16<1>::Vec *w, uint32_t ltab) {
     Tab<F> t0, t1;
     if constexpr (NT > 0) lds_tab_part<F>(t0, ltab, 0, 0, NQ);
     int have = 0;
+    int opi = 0;
+    (void)opi;
 #pragma unroll
     for (int i = 0; i < NS; i++) {
         const SStep st = sch.step[i];
@@ -753,7 +755,9 @@ __device__ __forceinline__ void run_split(F16<1>::Vec *w, uint32_t ltab) {
             __builtin_amdgcn_sched_barrier(0);
         }
         typename F::Vec &x = w[st.a], &y = w[st.b];
-        if (st.kind == OP_IFFT) {
+        if (RS_ABL_NO_MUL) {
+            F::xor_into(y, x);
+        } else if (st.kind == OP_IFFT) {
             F::xor_into(y, x);
             F::mul_add(x, y, t0.v);
         } else if (st.kind == OP_FFT) {
@@ -763,8 +767,12 @@ __device__ __forceinline__ void run_split(F16<1>::Vec *w, uint32_t ltab) {
             F::xor_into(y, x);
         }
 #if RS_SPLIT_PIN
-        F::pin(x);
-        F::pin(y);
+        // pin every RS_SPLIT_PIN-th op: bounds code motion (VGPRs) while letting
+        // consecutive independent butterflies interleave
+        if ((opi++ % RS_SPLIT_PIN) == RS_SPLIT_PIN - 1) {
+            F::pin(x);
+            F::pin(y);
+        }
 #endif
     }
 }
@@ -817,6 +825,7 @@ __global__ void __launch_bounds__(256, 4) k_encode_split(EncodeArgs a) {
     const uint32_t lane_off = (uint32_t)((lane >> 4) * a.data.stride) + (lane & 15) * 16 + span;
     auto stage_one = [&](int c, int j) {
         const int row0 = c * M, cnt = a.k - row0;
+        if (RS_ABL_NO_DMA) return;
         if (wave_full && cnt >= M) {
             const uint32_t so = (uint32_t)((uint64_t)(row0 + 4 * j) * a.data.stride);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(drsrc, (lvoid_t *)(img + j * 1024), 16, lane_off, so, 0, 0);
