@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stripes", type=int, default=8,
+                    help="stripes encoded per step (one launch); each is 128+32 x 1 MiB")
     args = ap.parse_args()
 
     import torch
@@ -88,7 +90,8 @@ def main():
     codec = rs.New16(K, P, device=dev.index)
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED + rank)
-    slab = torch.randint(0, 256, (1, K + P, S), dtype=torch.uint8, device=dev, generator=g)
+    B = args.stripes
+    slab = torch.randint(0, 256, (B, K + P, S), dtype=torch.uint8, device=dev, generator=g)
     stream = torch.cuda.current_stream()
 
     def barrier():
@@ -120,9 +123,9 @@ def main():
     el, kern_ms = float(t[0]), float(t[1])
 
     ms_per_step = el / args.steps * 1e3
-    data_bytes = world * args.steps * K * S
+    data_bytes = world * args.steps * B * K * S
     value = data_bytes / el / 2**30
-    alg_bytes = (K + P) * S
+    alg_bytes = B * (K + P) * S
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     kname = codec.encode_path
 

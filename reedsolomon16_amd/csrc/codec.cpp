@@ -29,6 +29,7 @@ using namespace rs;
 namespace {
 
 constexpr int kMaxRegLogM = 5;  // m <= 32: fused register kernel
+constexpr int kMaxLdsLogN = 8;  // n (or m) <= 256: LDS-resident transform kernels
 constexpr int kHostBufs = 3;    // staging slabs of the host-resident pipeline
 constexpr uint64_t kHostSegTarget = 8ull << 20;  // bytes copied in per segment
 
@@ -205,7 +206,8 @@ bool split_enabled() {
 // Host half of the encode plan (no device calls): twiddle schedule and panic check.
 void plan_encode_host(rs_codec *c) {
     c->enc_ok = encode_schedule(*c->F, c->k, c->p, c->enc_ifft_logs, c->enc_fft_logs, c->nchunks);
-    c->path = !c->enc_ok ? "panic" : (c->logm <= kMaxRegLogM ? encode_reg_name(c->bits, c->logm) : "multipass");
+    c->path = !c->enc_ok ? "panic" : (c->logm <= kMaxRegLogM ? encode_reg_name(c->bits, c->logm)
+                                                   : c->logm <= kMaxLdsLogN ? "lds-m" + std::to_string(c->m) : "multipass");
     if (c->enc_ok && c->bits == 16 && c->logm >= 2 && c->logm <= 5 && split_enabled())
         c->path = std::string("split16-m") + std::to_string(c->m);
 }
@@ -332,6 +334,22 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
         HIP_TRY(launch_encode_reg(c->bits, c->logm, mismatch != nullptr, a, s));
         return RS_OK;
     }
+    if (c->logm <= kMaxLdsLogN) {  // m rows of accumulator + chunk LDS-resident
+        EncodeArgs a{};
+        a.data = data;
+        a.parity = par;
+        a.k = c->k;
+        a.p = c->p;
+        a.nchunks = c->nchunks;
+        a.shard_size = S;
+        a.stripe_stride = (data.table || par.table) ? 0 : stripe_stride;
+        a.nstripes = (data.table || par.table) ? 1 : nstripes;
+        a.tw_ifft = c->tw_ifft.p;
+        a.tw_fft = c->tw_fft.p;
+        a.mismatch = mismatch;
+        HIP_TRY(launch_encode_lds(c->bits, c->logm, mismatch != nullptr, a, s));
+        return RS_OK;
+    }
     for (int j = 0; j < nstripes; j++) {
         RowSet d = data, p = par;
         if (!d.table) d.base += (size_t)j * stripe_stride;
@@ -430,6 +448,22 @@ int upload_reconstruct(rs_codec *c, const RecPlan &pl, const std::vector<uint8_t
 // Device work of one reconstruct over row-pointer set `set` of the uploaded plan.
 int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipStream_t s) {
     const int n = c->n, nd = (int)pl.dst_shard.size();
+    if (c->logn <= kMaxLdsLogN) {  // whole transform LDS-resident: one HBM read/write per row
+        if (!nd) return RS_OK;
+        RecArgs ra{};
+        ra.src = c->rc_src.p + (size_t)set * n;
+        ra.dst = c->rc_dst.p + (size_t)set * nd;
+        ra.pos = c->rc_pos.p;
+        ra.tw_in = c->rc_tw_in.p;
+        ra.tw_out = c->rc_tw_out.p;
+        ra.tw_ifft = c->dtw_ifft.p;
+        ra.tw_fft = c->dtw_fft.p;
+        ra.S = S;
+        ra.mtrunc = c->m + c->k;
+        ra.nd = nd;
+        HIP_TRY(launch_rec_lds(c->bits, c->logn, ra, s));
+        return RS_OK;
+    }
     HIP_TRY(c->work.ensure((size_t)n * S));
     uint8_t *w = c->work.p;
     HIP_TRY(launch_scale_in(c->bits, w, S, c->rc_src.p + (size_t)set * n, c->rc_tw_in.p, n, s));

@@ -34,6 +34,10 @@
 #define RS_ABL_NO_MUL 0
 #endif
 // RS_ABL_TAB_ONCE: fused encode reads one twiddle table per transform (wrong results)
+// RS_ABL_NOSWAP: split kernel skips its permlane32 swaps (wrong results)
+#ifndef RS_ABL_NOSWAP
+#define RS_ABL_NOSWAP 0
+#endif
 #ifndef RS_ABL_TAB_ONCE
 #define RS_ABL_TAB_ONCE 0
 #endif
@@ -730,6 +734,7 @@ __device__ __forceinline__ void run_split(F16<1>::Vec *w, uint32_t ltab) {
     for (int i = 0; i < NS; i++) {
         const SStep st = sch.step[i];
         if (st.type == ST_SWAP) {
+            if (RS_ABL_NOSWAP) continue;
             const auto rl = __builtin_amdgcn_permlane32_swap(w[st.a].l[0], w[st.b].l[0], false, false);
             const auto rh = __builtin_amdgcn_permlane32_swap(w[st.a].h[0], w[st.b].h[0], false, false);
             w[st.a].l[0] = rl[0];
@@ -1112,6 +1117,285 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------- LDS-resident transforms (n <= 256)
+// One workgroup owns a 128-byte tile (two 64-byte blocks) of every row and
+// keeps all n rows of it in LDS for the whole operation, so HBM sees each
+// input row once and each output row once (the multi-pass path above re-reads
+// the n-row work slab on every radix-4 layer).  Used for reconstruct
+// (leopard16.go:390-570 / leopard8.go:439-695: scale-in, IFFT over n rows,
+// formal derivative, FFT, reveal) and for encode with 32 < m <= 256
+// (leopard16.go:128-224: chunked IFFT-m + XOR + FFT-m).
+// Lane work items are (row group, unit) pairs; units are F16<4> (16 symbols:
+// 16 low bytes + the 16 high bytes 32 bytes later) or F8<4> (16 bytes).
+// Twiddle tables come from global memory (identical for every workgroup, so
+// they stay in L1/L2).
+constexpr int kTileB = 128;   // bytes of each row owned by a workgroup
+constexpr int kLdsRow = 144;  // LDS row stride: 36 dwords spreads rows over the banks
+
+template <class F>
+struct LTile {
+    static constexpr bool W16 = F::TWD == 24;
+    static constexpr int UB = W16 ? 8 * F::W : 4 * F::W;  // global bytes per unit
+    static constexpr int U = kTileB / UB;                 // units per tile
+    typedef typename F::Vec V;
+    __device__ static V get(const uint8_t *lds, int row, int u) {
+        V v;
+        const uint8_t *p = lds + row * kLdsRow + F::off(u);
+        if constexpr (W16) {
+            ldw_lds<F::W>(p, v.l);
+            ldw_lds<F::W>(p + 32, v.h);
+        } else {
+            ldw_lds<F::W>(p, v.b);
+        }
+        return v;
+    }
+    __device__ static void put(uint8_t *lds, int row, int u, const V &v) {
+        typedef typename VecOf<F::W>::T T;
+        uint8_t *p = lds + row * kLdsRow + F::off(u);
+        auto st = [](uint8_t *q, const uint32_t(&w)[F::W]) {
+            T x;
+            if constexpr (F::W == 1) x = w[0];
+            else
+#pragma unroll
+                for (int i = 0; i < F::W; i++) x[i] = w[i];
+            *(__attribute__((address_space(3))) T *)(q) = x;
+        };
+        if constexpr (W16) {
+            st(p, v.l);
+            st(p + 32, v.h);
+        } else {
+            st(p, v.b);
+        }
+    }
+    // Unit u of the tile starting at byte `tile` exists in a row of S bytes.
+    __device__ static bool valid(uint64_t tile, uint64_t S, int u) { return tile + (uint64_t)(F::off(u) & ~63) < S; }
+};
+
+// One radix-4 pass (rows i, i+d, i+2d, i+3d; twiddles m01, m02, m23 at
+// tw + 3*g) over the active groups, or a radix-2 pass, on the LDS rows.
+template <class F, bool INV>
+__device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int groups_active,
+                                         const uint32_t *__restrict__ tw) {
+    typedef LTile<F> L;
+    typedef typename F::Vec V;
+    constexpr int U = L::U;
+    if (radix == 4) {
+        const int items = groups_active * dist * U;
+        for (int it = threadIdx.x; it < items; it += 256) {
+            const int q = it / U, u = it - q * U;
+            const int g = q / dist, j = q - g * dist;
+            const int i = g * 4 * dist + j;
+            const uint32_t *t = tw + (uint64_t)g * 3 * F::TWD;
+            V x0 = L::get(lds, i, u), x1 = L::get(lds, i + dist, u), x2 = L::get(lds, i + 2 * dist, u),
+              x3 = L::get(lds, i + 3 * dist, u);
+            if constexpr (INV) ifft4<F>(x0, x1, x2, x3, t);
+            else fft4<F>(x0, x1, x2, x3, t);
+            L::put(lds, i, u, x0);
+            L::put(lds, i + dist, u, x1);
+            L::put(lds, i + 2 * dist, u, x2);
+            L::put(lds, i + 3 * dist, u, x3);
+        }
+    } else {
+        // inverse: pairs (j, j + dist), j < dist, one twiddle; forward: dist 1, pairs (2g, 2g+1), twiddle g
+        const int pairs = INV ? dist : groups_active;
+        for (int it = threadIdx.x; it < pairs * U; it += 256) {
+            const int q = it / U, u = it - q * U;
+            const int rx = INV ? q : 2 * q, ry = INV ? q + dist : 2 * q + 1;
+            const uint32_t *t = INV ? tw : tw + (uint64_t)q * F::TWD;
+            V x = L::get(lds, rx, u), y = L::get(lds, ry, u);
+            if constexpr (INV) ifft2<F>(x, y, t);
+            else fft2<F>(x, y, t);
+            L::put(lds, rx, u, x);
+            L::put(lds, ry, u, y);
+        }
+    }
+    __syncthreads();
+}
+
+// Full transform over 2^LOGN LDS rows with the reference's pass structure
+// (gf_host.cpp ifft_passes / fft_passes) and its mtrunc group skipping.
+template <class F, bool INV, int LOGN>
+__device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw) {
+    constexpr int N = 1 << LOGN;
+    int slot = 0;
+    if constexpr (INV) {
+        int dist = 1;
+        for (; dist * 4 <= N; dist *= 4) {
+            const int groups = N / (4 * dist);
+            int active = (mtrunc + 4 * dist - 1) / (4 * dist);
+            if (active > groups) active = groups;
+            lds_pass<F, true>(lds, dist, 4, active, tw + (uint64_t)slot * F::TWD);
+            slot += 3 * groups;
+        }
+        if (dist < N) lds_pass<F, true>(lds, dist, 2, 1, tw + (uint64_t)slot * F::TWD);
+    } else {
+        int dist = N / 4;
+        for (; dist != 0; dist /= 4) {
+            const int groups = N / (4 * dist);
+            int active = (mtrunc + 4 * dist - 1) / (4 * dist);
+            if (active > groups) active = groups;
+            lds_pass<F, false>(lds, dist, 4, active, tw + (uint64_t)slot * F::TWD);
+            slot += 3 * groups;
+        }
+        if (LOGN & 1) {
+            int active = (mtrunc + 1) / 2;
+            if (active > N / 2) active = N / 2;
+            lds_pass<F, false>(lds, 1, 2, active, tw + (uint64_t)slot * F::TWD);
+        }
+    }
+}
+
+// Reconstruct (leopard16.go:432-568) of one stripe, one 128-byte tile per workgroup.
+template <class F, int LOGN>
+__global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
+    typedef LTile<F> L;
+    typedef typename F::Vec V;
+    constexpr int N = 1 << LOGN, U = L::U;
+    constexpr int K = (N * U + 255) / 256;  // derivative outputs per thread
+    __shared__ __attribute__((aligned(16))) uint8_t lds[N * kLdsRow];
+    const uint64_t tile = (uint64_t)blockIdx.x * kTileB;
+    // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0
+    for (int it = threadIdx.x; it < N * U; it += 256) {
+        const int r = it / U, u = it - r * U;
+        V v = F::zero();
+        const uint8_t *src = a.src[r];
+        if (src && L::valid(tile, a.S, u)) F::mul_add(v, F::load(src + tile, u), a.tw_in + (uint64_t)r * F::TWD);
+        L::put(lds, r, u, v);
+    }
+    __syncthreads();
+    lds_transform<F, true, LOGN>(lds, a.mtrunc, a.tw_ifft);
+    // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
+    {
+        V o[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int it = threadIdx.x + 256 * k;
+            if (it < N * U) {
+                const int r = it / U, u = it - r * U;
+                o[k] = L::get(lds, r, u);
+                for (int b = 1; b < N; b <<= 1)
+                    if (!(r & b)) F::xor_into(o[k], L::get(lds, r | b, u));
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int it = threadIdx.x + 256 * k;
+            if (it < N * U) {
+                const int r = it / U, u = it - r * U;
+                L::put(lds, r, u, o[k]);
+            }
+        }
+        __syncthreads();
+    }
+    lds_transform<F, false, LOGN>(lds, a.mtrunc, a.tw_fft);
+    // reveal: shard = work[pos] * (modulus - errLocs[pos])
+    for (int it = threadIdx.x; it < a.nd * U; it += 256) {
+        const int j = it / U, u = it - j * U;
+        if (!L::valid(tile, a.S, u)) continue;
+        V v = F::zero();
+        F::mul_add(v, L::get(lds, a.pos[j], u), a.tw_out + (uint64_t)j * F::TWD);
+        F::store(a.dst[j] + tile, u, v);
+    }
+}
+
+// Encode for 32 < m <= 256 (leopard16.go:128-224 / leopard8.go:153-277):
+// acc and the current chunk both live in LDS (2 x m rows of the tile).
+template <class F, int LOGM, bool VERIFY>
+__global__ void __launch_bounds__(256) k_enc_lds(EncodeArgs a) {
+    typedef LTile<F> L;
+    typedef typename F::Vec V;
+    constexpr int M = 1 << LOGM, U = L::U;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
+    uint8_t *acc = lds_dyn, *cur = lds_dyn + M * kLdsRow;
+    const uint64_t tile = (uint64_t)blockIdx.x * kTileB;
+    const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
+    constexpr int its = ifft_slot_count(LOGM);
+    for (int c = 0; c < a.nchunks; c++) {
+        const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
+        uint8_t *dst = c == 0 ? acc : cur;
+        for (int it = threadIdx.x; it < M * U; it += 256) {
+            const int r = it / U, u = it - r * U;
+            V v = F::zero();
+            if (r < cnt && L::valid(tile, a.shard_size, u)) v = F::load(row_ptr(a.data, row0 + r) + soff + tile, u);
+            L::put(dst, r, u, v);
+        }
+        __syncthreads();
+        lds_transform<F, true, LOGM>(dst, cnt, a.tw_ifft + (uint64_t)c * its * F::TWD);
+        if (c > 0) {
+            for (int it = threadIdx.x; it < M * U; it += 256) {
+                const int r = it / U, u = it - r * U;
+                V x = L::get(acc, r, u);
+                F::xor_into(x, L::get(cur, r, u));
+                L::put(acc, r, u, x);
+            }
+            __syncthreads();
+        }
+    }
+    lds_transform<F, false, LOGM>(acc, a.p, a.tw_fft);
+    uint32_t bad = 0;
+    for (int it = threadIdx.x; it < a.p * U; it += 256) {
+        const int r = it / U, u = it - r * U;
+        if (!L::valid(tile, a.shard_size, u)) continue;
+        uint8_t *prow = row_ptr(a.parity, r) + soff + tile;
+        const V v = L::get(acc, r, u);
+        if constexpr (VERIFY) bad |= F::diff(v, F::load(prow, u));
+        else F::store(prow, u, v);
+    }
+    if constexpr (VERIFY) {
+        if (bad) flag_mismatch(a.mismatch);
+    }
+}
+
+template <class F, int LOGN>
+hipError_t rec_lds_t(const RecArgs &a, hipStream_t s) {
+    const dim3 grid((unsigned)((a.S + kTileB - 1) / kTileB));
+    hipLaunchKernelGGL((k_rec_lds<F, LOGN>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+template <class F>
+hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
+    switch (logn) {
+        case 1: return rec_lds_t<F, 1>(a, s);
+        case 2: return rec_lds_t<F, 2>(a, s);
+        case 3: return rec_lds_t<F, 3>(a, s);
+        case 4: return rec_lds_t<F, 4>(a, s);
+        case 5: return rec_lds_t<F, 5>(a, s);
+        case 6: return rec_lds_t<F, 6>(a, s);
+        case 7: return rec_lds_t<F, 7>(a, s);
+        case 8: return rec_lds_t<F, 8>(a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <class F, int LOGM>
+hipError_t enc_lds_t(bool verify, const EncodeArgs &a, hipStream_t s) {
+    const dim3 grid((unsigned)((a.shard_size + kTileB - 1) / kTileB), (unsigned)a.nstripes);
+    const size_t lds = (size_t)2 * (1 << LOGM) * kLdsRow;
+    if (verify) {
+        (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_enc_lds<F, LOGM, true>), grid, dim3(256), lds, s, a);
+    } else {
+        (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_enc_lds<F, LOGM, false>), grid, dim3(256), lds, s, a);
+    }
+    return hipGetLastError();
+}
+template <class F>
+hipError_t enc_lds_f(int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
+    switch (logm) {
+        case 2: return enc_lds_t<F, 2>(verify, a, s);
+        case 3: return enc_lds_t<F, 3>(verify, a, s);
+        case 4: return enc_lds_t<F, 4>(verify, a, s);
+        case 5: return enc_lds_t<F, 5>(verify, a, s);
+        case 6: return enc_lds_t<F, 6>(verify, a, s);
+        case 7: return enc_lds_t<F, 7>(verify, a, s);
+        case 8: return enc_lds_t<F, 8>(verify, a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
 }  // namespace
 
 // Lane width per (field, log2 m): keep acc + work + prefetch <= ~192 VGPRs
@@ -1247,6 +1531,15 @@ hipError_t launch_reveal(int bits, uint8_t *const *dst, const uint8_t *work, uin
         else
             hipLaunchKernelGGL(k_reveal<F8<4>>, dim3(grid_x(S / 16).x, ny), dim3(256), 0, s, dst, work, S, pos, tw, y0);
     });
+}
+
+
+hipError_t launch_rec_lds(int bits, int logn, const RecArgs &a, hipStream_t s) {
+    return bits == 16 ? rec_lds_f<F16<4>>(logn, a, s) : rec_lds_f<F8<4>>(logn, a, s);
+}
+
+hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
+    return bits == 16 ? enc_lds_f<F16<4>>(logm, verify, a, s) : enc_lds_f<F8<4>>(logm, verify, a, s);
 }
 
 }  // namespace rs

@@ -62,4 +62,23 @@ hipError_t launch_formal_derivative(int bits, uint8_t *work, uint64_t S, int n, 
 hipError_t launch_reveal(int bits, uint8_t *const *dst, const uint8_t *work, uint64_t S, const int *pos,
                          const uint32_t *tw, int count, hipStream_t s);
 
+
+// ---- LDS-resident paths: one workgroup per 128-byte tile of every row ----
+// Reconstruct of one stripe over n = 2^logn <= 256 work rows.
+struct RecArgs {
+    const uint8_t *const *src;  // n device row pointers (nullptr: zero row)
+    uint8_t *const *dst;        // nd output rows
+    const int *pos;             // work row of each output
+    const uint32_t *tw_in;      // n tables: errLocs scalings (mulgf16 semantics)
+    const uint32_t *tw_out;     // nd tables: modulus - errLocs[pos]
+    const uint32_t *tw_ifft;    // decoder IFFT schedule (ifft_slots(logn) tables)
+    const uint32_t *tw_fft;     // decoder FFT schedule (fft_slots(logn) tables)
+    uint64_t S;
+    int mtrunc;                 // m + k
+    int nd;
+};
+hipError_t launch_rec_lds(int bits, int logn, const RecArgs &a, hipStream_t s);
+// Encode (or verify) for 2 <= logm <= 8, twiddles as for launch_encode_reg.
+hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
+
 }  // namespace rs

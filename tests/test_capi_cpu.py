@@ -130,7 +130,8 @@ def test_constructor_errors():
     assert rs.New(200, 100).field_bits == 16
     assert rs.New16(128, 32).encode_path == "split16-m32"
     assert rs.New16(10, 1).encode_path == "reg16-m1"
-    assert rs.New16(1024, 256).encode_path == "multipass"
+    assert rs.New16(1024, 256).encode_path == "lds-m256"
+    assert rs.New16(1024, 300).encode_path == "multipass"
 
 
 def test_host_validation_errors_without_device():
