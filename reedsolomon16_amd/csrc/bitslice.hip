@@ -1,0 +1,375 @@
+// Bit-sliced GF(2^16) encode for m = 32 (gfx950), specialized per geometry.
+//
+// Why: multiplying by a twiddle with v_perm_b32 byte tables costs ~115 SIMD
+// cycles per 4 symbols (12 half-rate v_perm_b32 + extraction + XOR folding,
+// scripts/micro/split_rate.hip), which caps the table-driven kernels at ~45 us
+// of pure VALU for C3.  In bit-sliced form (a 32-bit word holds one bit of 32
+// symbols) a multiply by a *known* constant is a fixed XOR network: output
+// plane i = XOR of the input planes in row i of the twiddle's 16x16 GF(2)
+// matrix -- about 50 full-rate v_bitop3_b32 per 32 symbols.  The matrices
+// are generated at build time for the geometries listed in the Makefile
+// (tools/gen_bs_tables.cpp -> build/bs_tables.h), so every twiddle is an
+// instruction-stream constant.
+//
+// Work split (one 512-thread workgroup per CU, persistent over tiles): a tile
+// is 64 adjacent 64-byte blocks (4 KB) of every row of one stripe; lane l owns
+// block l (32 symbols) in every wave.  The 8 waves split the 32 rows of a
+// transform; each radix-4 pass runs in registers on the 4 rows a wave holds,
+// and the passes exchange rows through a 32-row bit-sliced LDS image (128 KB).
+// A wave's role (which rows, hence which twiddles) is its wave index, a
+// wave-uniform value: every role has its own instruction stream.
+//
+//   chunk IFFT (leopard16.go:694-741):  pass 1 rows 4w+{0..3} (dist 1, 2)
+//                                        pass 2 rows 16h+j+{0,4,8,12} (dist 4, 8)
+//                                        pass 3 rows w+{0,8,16,24} (dist 16)
+//   accumulator rows w+{0,8,16} stay in registers across chunks, row w+24 in
+//   a private LDS row of the wave;
+//   final FFT (leopard16.go:618-657):   pass A rows w+{0,8,16,24} (dist 16, 8)
+//                                        pass B rows 8g+j+{0,2,4,6} (dist 4, 2)
+//                                        pass C rows 4w+{0..3} (dist 1)
+// HBM: each data row read once, each parity row written once; the next
+// chunk's rows are prefetched into registers during the current chunk.
+//
+// Register budget (2 waves per SIMD -> 256 VGPRs): 64 staged + 64 working +
+// 48 accumulator.  The XOR networks are written as in-place inline asm so the
+// compiler cannot rename their intermediates into fresh registers, and every
+// butterfly and chunk is a scheduling region of its own.
+#include <utility>
+
+#include "bs_tables.h"
+#include "kernels.hpp"
+
+namespace rs {
+namespace {
+
+typedef uint32_t Planes[16];
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// v ^= a  /  v ^= a ^ b, in place (v_bitop3_b32 truth table 0x96 = 3-input XOR).
+__device__ __forceinline__ void ixor(uint32_t &v, uint32_t a) { asm("v_xor_b32 %0, %1, %0" : "+v"(v) : "v"(a)); }
+__device__ __forceinline__ void ixor3(uint32_t &v, uint32_t a, uint32_t b) {
+    asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(v) : "v"(a), "v"(b));
+}
+
+// Delta swap of word-index bit k with bit-position bit k (s = 2^k, M = positions with bit k clear).
+__device__ __forceinline__ void bs_xchg(uint32_t &a, uint32_t &b, int s, uint32_t M) {
+    const uint32_t as = a >> s, bsh = b << s;
+    a = (a & M) | (bsh & ~M);
+    b = (b & ~M) | (as & M);
+}
+// A 64-byte block (dwords 0-7: low bytes of symbols 4w+j at byte j of dword w;
+// dwords 8-15: high bytes) <-> 16 bit-planes (plane b bit 8j+w = bit b of symbol
+// 4w+j; planes 8-15 from the high bytes).  An involution.
+__device__ __forceinline__ void bs_transpose(Planes &w) {
+#pragma unroll
+    for (int h = 0; h < 16; h += 8)
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int s = 1 << k;
+            const uint32_t M = k == 0 ? 0x55555555u : k == 1 ? 0x33333333u : 0x0F0F0F0Fu;
+#pragma unroll
+            for (int a = 0; a < 8; a++)
+                if (!(a & s)) bs_xchg(w[h + a], w[h + a + s], s, M);
+        }
+}
+
+__device__ __forceinline__ void xor16(Planes &y, const Planes &x) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) ixor(y[i], x[i]);
+}
+
+// x ^= y * twiddle (C >= 0: chunk C's IFFT slot; C < 0: FFT slot).
+// Each output plane is a chain of 3-input XORs over the input planes its
+// matrix row selects.
+template <class TW, int C, int SLOT>
+__device__ __forceinline__ void bs_mul_add(Planes &x, const Planes &y) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const uint32_t r = C < 0 ? TW::fft[SLOT][i] : TW::ifft[C < 0 ? 0 : C][SLOT][i];
+        int pend = -1;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            if ((r >> j) & 1) {
+                if (pend < 0) {
+                    pend = j;
+                } else {
+                    ixor3(x[i], y[pend], y[j]);
+                    pend = -1;
+                }
+            }
+        }
+        if (pend >= 0) ixor(x[i], y[pend]);
+    }
+}
+// IFFT butterfly: y ^= x; x ^= y * t.   FFT butterfly: x ^= y * t; y ^= x.
+// Each butterfly is a scheduling region of its own (sched_barrier): the
+// machine scheduler would otherwise interleave butterflies for ILP and run
+// the kernel out of registers.
+template <class TW, int C, int SLOT>
+__device__ __forceinline__ void bs_ifft2(Planes &x, Planes &y) {
+    xor16(y, x);
+    bs_mul_add<TW, C, SLOT>(x, y);
+    __builtin_amdgcn_sched_barrier(0);
+}
+template <class TW, int SLOT>
+__device__ __forceinline__ void bs_fft2(Planes &x, Planes &y) {
+    bs_mul_add<TW, -1, SLOT>(x, y);
+    xor16(y, x);
+    __builtin_amdgcn_sched_barrier(0);
+}
+// Radix-4 groups with slots (m01, m02, m23) = (S0, S0+1, S0+2).
+template <class TW, int C, int S0>
+__device__ __forceinline__ void bs_ifft4(Planes (&r)[4]) {
+    bs_ifft2<TW, C, S0>(r[0], r[1]);
+    bs_ifft2<TW, C, S0 + 2>(r[2], r[3]);
+    bs_ifft2<TW, C, S0 + 1>(r[0], r[2]);
+    bs_ifft2<TW, C, S0 + 1>(r[1], r[3]);
+}
+template <class TW, int S0>
+__device__ __forceinline__ void bs_fft4(Planes (&r)[4]) {
+    bs_fft2<TW, S0 + 1>(r[0], r[2]);
+    bs_fft2<TW, S0 + 1>(r[1], r[3]);
+    bs_fft2<TW, S0>(r[0], r[1]);
+    bs_fft2<TW, S0 + 2>(r[2], r[3]);
+}
+
+// Wave-uniform dispatch of a role-specialized pass: f(std::integral_constant<int, R>) for R = role.
+template <int N, class Fn, int... Is>
+__device__ __forceinline__ void dispatch_impl(int role, Fn &&f, std::integer_sequence<int, Is...>) {
+    ((role == Is ? (f(std::integral_constant<int, Is>{}), 0) : 0), ...);
+}
+template <int N, class Fn>
+__device__ __forceinline__ void dispatch(int role, Fn &&f) {
+    dispatch_impl<N>(role, f, std::make_integer_sequence<int, N>{});
+}
+
+// LDS image: row r, plane quad q of lane l at dword r*1024 + q*256 + l*4.
+typedef __attribute__((address_space(3))) u32x4 lds_u4;
+// The row address is rebuilt at every use from an opaque copy of the lane base
+// (one v_add): otherwise the compiler hoists every row address out of the
+// persistent tile loop and spills them.
+__device__ __forceinline__ uint32_t row_addr(uint32_t lbase, int row) {
+    uint32_t b = lbase;
+    asm volatile("" : "+v"(b));
+    return b + (uint32_t)row * 4096u;
+}
+__device__ __forceinline__ void lds_put(uint32_t lbase, int row, const Planes &v) {
+    const uint32_t ra = row_addr(lbase, row);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        *(lds_u4 *)(uintptr_t)(ra + q * 1024) = u32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+}
+__device__ __forceinline__ void lds_get(uint32_t lbase, int row, Planes &v) {
+    const uint32_t ra = row_addr(lbase, row);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const u32x4 x = *(const lds_u4 *)(uintptr_t)(ra + q * 1024);
+        v[4 * q] = x[0];
+        v[4 * q + 1] = x[1];
+        v[4 * q + 2] = x[2];
+        v[4 * q + 3] = x[3];
+    }
+}
+
+typedef __attribute__((address_space(1))) const u32x4 gc_u4;
+typedef __attribute__((address_space(1))) u32x4 g_u4;
+
+template <class TW, bool VERIFY>
+struct BsEncoder {
+    static constexpr int NCH = TW::NCH;
+    const BsArgs &a;
+    uint32_t lbase;  // this lane's LDS byte address of row 0, quad 0
+    int lane, w;
+    Planes St[4];    // staged data rows (64-byte blocks as loaded)
+    Planes R[4];     // working rows (bit-planes)
+    Planes A[3];     // accumulator rows w, w + 8, w + 16 (row w + 24's: LDS row 32 + w)
+
+    // Load rows 32c + 4w + i of `tile` (zero past k, past the row end, past the last tile).
+    __device__ __forceinline__ void stage(int tile, int c) {
+        const int tps = a.tiles_per_stripe;
+        const int stripe = tile / tps, ct = tile - stripe * tps;
+        const uint64_t col = (uint64_t)ct * 4096 + (uint64_t)lane * 64;
+        const bool ok = tile < a.ntiles && col < a.S;
+        const uint8_t *base = a.data + (uint64_t)stripe * a.stripe_stride + col;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = 32 * c + 4 * w + i;
+            if (ok && row < a.k) {
+                gc_u4 *p = (gc_u4 *)(base + (uint64_t)row * a.row_stride);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const u32x4 x = p[q];
+                    St[i][4 * q] = x[0];
+                    St[i][4 * q + 1] = x[1];
+                    St[i][4 * q + 2] = x[2];
+                    St[i][4 * q + 3] = x[3];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16; q++) St[i][q] = 0;
+            }
+        }
+    }
+
+    template <int C>
+    __device__ __forceinline__ void chunk(int tile) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+#pragma unroll
+            for (int q = 0; q < 16; q++) R[i][q] = St[i][q];
+            bs_transpose(R[i]);
+        }
+        // the staged rows are dead before the next chunk's loads reuse their registers
+        __builtin_amdgcn_sched_barrier(0);
+        if (C + 1 < NCH) stage(tile, C + 1);
+        else stage(tile + (int)gridDim.x, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        // pass 1: rows 4w + i, radix-4 at dist 1 (group w, slots 3w..3w+2)
+        dispatch<8>(w, [&](auto W) { bs_ifft4<TW, C, 3 * decltype(W)::value>(R); });
+        __syncthreads();  // previous readers of the image are done
+#pragma unroll
+        for (int i = 0; i < 4; i++) lds_put(lbase, 4 * w + i, R[i]);
+        __syncthreads();
+        // pass 2: rows 16h + j + 4i, radix-4 at dist 4 (group h, slots 24 + 3h ..)
+        const int h = w >> 2, j = w & 3;
+#pragma unroll
+        for (int i = 0; i < 4; i++) lds_get(lbase, 16 * h + j + 4 * i, R[i]);
+        dispatch<2>(h, [&](auto H) { bs_ifft4<TW, C, 24 + 3 * decltype(H)::value>(R); });
+#pragma unroll
+        for (int i = 0; i < 4; i++) lds_put(lbase, 16 * h + j + 4 * i, R[i]);
+        __syncthreads();
+        // pass 3: rows w + 8i, radix-2 at dist 16 (slot 30): pairs (w, w+16), (w+8, w+24)
+#pragma unroll
+        for (int i = 0; i < 4; i++) lds_get(lbase, w + 8 * i, R[i]);
+        bs_ifft2<TW, C, 30>(R[0], R[2]);
+        bs_ifft2<TW, C, 30>(R[1], R[3]);
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            if (C == 0) {
+#pragma unroll
+                for (int q = 0; q < 16; q++) A[i][q] = R[i][q];
+            } else {
+                xor16(A[i], R[i]);
+            }
+        }
+        // the fourth accumulator row lives in this wave's private LDS row
+        if (C == 0) {
+            lds_put(lbase, 32 + w, R[3]);
+        } else {
+            lds_get(lbase, 32 + w, R[0]);
+            xor16(R[0], R[3]);
+            lds_put(lbase, 32 + w, R[0]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    template <int... Cs>
+    __device__ __forceinline__ void chunks(int tile, std::integer_sequence<int, Cs...>) {
+        (chunk<Cs>(tile), ...);
+    }
+
+    __device__ __forceinline__ void run() {
+        int tile = blockIdx.x;
+        stage(tile, 0);
+        for (; tile < a.ntiles; tile += gridDim.x) {
+            chunks(tile, std::make_integer_sequence<int, NCH>{});
+            // FFT pass A: rows w + 8i (dist 16 then 8; the only group: slots 0..2)
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int q = 0; q < 16; q++) R[i][q] = A[i][q];
+            lds_get(lbase, 32 + w, R[3]);
+            bs_fft4<TW, 0>(R);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 4; i++) lds_put(lbase, w + 8 * i, R[i]);
+            __syncthreads();
+            // pass B: rows 8g + j + 2i (dist 4 then 2; group g, slots 3 + 3g ..)
+            const int g = w >> 1, j = w & 1;
+#pragma unroll
+            for (int i = 0; i < 4; i++) lds_get(lbase, 8 * g + j + 2 * i, R[i]);
+            dispatch<4>(g, [&](auto G) { bs_fft4<TW, 3 + 3 * decltype(G)::value>(R); });
+#pragma unroll
+            for (int i = 0; i < 4; i++) lds_put(lbase, 8 * g + j + 2 * i, R[i]);
+            __syncthreads();
+            // pass C: rows 4w + i, radix-2 at dist 1 (slots 15 + 2w, 16 + 2w)
+#pragma unroll
+            for (int i = 0; i < 4; i++) lds_get(lbase, 4 * w + i, R[i]);
+            dispatch<8>(w, [&](auto W) {
+                constexpr int s = 15 + 2 * decltype(W)::value;
+                bs_fft2<TW, s>(R[0], R[1]);
+                bs_fft2<TW, s + 1>(R[2], R[3]);
+            });
+            // parity rows 4w + i < p
+            const int tps = a.tiles_per_stripe;
+            const int stripe = tile / tps, ct = tile - stripe * tps;
+            const uint64_t col = (uint64_t)ct * 4096 + (uint64_t)lane * 64;
+            uint32_t bad = 0;
+            if (col < a.S) {
+                uint8_t *base = a.parity + (uint64_t)stripe * a.stripe_stride + col;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int row = 4 * w + i;
+                    if (row >= a.p) continue;
+                    bs_transpose(R[i]);
+                    g_u4 *q = (g_u4 *)(base + (uint64_t)row * a.row_stride);
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const u32x4 v = u32x4{R[i][4 * k], R[i][4 * k + 1], R[i][4 * k + 2], R[i][4 * k + 3]};
+                        if constexpr (VERIFY) {
+                            const u32x4 o = q[k];
+                            bad |= (o[0] ^ v[0]) | (o[1] ^ v[1]) | (o[2] ^ v[2]) | (o[3] ^ v[3]);
+                        } else {
+                            q[k] = v;
+                        }
+                    }
+                }
+            }
+            if constexpr (VERIFY) {
+                // one system-scope store per wave, not per lane (the flag word is host-mapped)
+                const uint64_t m = __ballot(bad != 0);
+                if (m && lane == __ffsll((unsigned long long)m) - 1)
+                    __hip_atomic_store(a.mismatch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+};
+
+template <class TW, bool VERIFY>
+__global__ void __launch_bounds__(512, 2) k_encode_bs(BsArgs a) {
+    // 32 image rows + 8 per-wave accumulator rows, each 64 blocks x 16 planes (160 KB)
+    __shared__ __attribute__((aligned(16))) uint32_t lds[40 * 1024];
+    BsEncoder<TW, VERIFY> e{a};
+    e.lane = threadIdx.x & 63;
+    e.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    e.lbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)lds + e.lane * 16;
+    e.run();
+}
+
+template <class TW>
+hipError_t launch_bs_t(bool verify, const BsArgs &a, int grid, hipStream_t s) {
+    if (verify) hipLaunchKernelGGL((k_encode_bs<TW, true>), dim3(grid), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((k_encode_bs<TW, false>), dim3(grid), dim3(512), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool encode_bs_available(int k, int p) {
+#define RS_BS_HAS(K, P) \
+    if (k == K && p == P) return true;
+    RS_BS_CONFIGS(RS_BS_HAS)
+#undef RS_BS_HAS
+    return false;
+}
+
+hipError_t launch_encode_bs(bool verify, const BsArgs &a, int grid, hipStream_t s) {
+#define RS_BS_LAUNCH(K, P) \
+    if (a.k == K && a.p == P) return launch_bs_t<BsTw<K, P>>(verify, a, grid, s);
+    RS_BS_CONFIGS(RS_BS_LAUNCH)
+#undef RS_BS_LAUNCH
+    return hipErrorNotSupported;
+}
+
+}  // namespace rs

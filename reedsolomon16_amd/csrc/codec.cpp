@@ -88,6 +88,8 @@ struct rs_codec {
     std::vector<uint32_t> enc_ifft_logs, enc_fft_logs;
     DevBuf<uint32_t> tw_ifft, tw_fft;
     bool split_ok = false;            // half-wave split kernel available (GF(2^16), 4 <= m <= 32)
+    bool bs_ok = false;               // bit-sliced kernel compiled in for (k, p) (GF(2^16), m = 32)
+    int cus = 0;                      // compute units of the device (persistent grids)
     DevBuf<uint32_t> tws_ifft, tws_fft;  // its twiddle images (schedule.hpp EncodeSplit)
     std::string path;
 
@@ -197,6 +199,12 @@ int upload_split(rs_codec *c) {
     return RS_OK;
 }
 
+// The bit-sliced kernel is opt-in (RS_BS=1) until it is parity-green on the GPU.
+bool bs_enabled() {
+    const char *e = getenv("RS_BS");
+    return e && e[0] == '1';
+}
+
 // RS_NO_SPLIT=1 disables the split kernel (A/B experiments only).
 bool split_enabled() {
     const char *e = getenv("RS_NO_SPLIT");
@@ -210,6 +218,8 @@ void plan_encode_host(rs_codec *c) {
                                                    : c->logm <= kMaxLdsLogN ? "lds-m" + std::to_string(c->m) : "multipass");
     if (c->enc_ok && c->bits == 16 && c->logm >= 2 && c->logm <= 5 && split_enabled())
         c->path = std::string("split16-m") + std::to_string(c->m);
+    c->bs_ok = c->enc_ok && c->bits == 16 && c->logm == 5 && bs_enabled() && encode_bs_available(c->k, c->p);
+    if (c->bs_ok) c->path = "bs16-m32";
 }
 
 // Device half, on first use: stream, flag word, encode twiddle tables.
@@ -323,6 +333,24 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
         a.tw_ifft = c->tw_ifft.p;
         a.tw_fft = c->tw_fft.p;
         a.mismatch = mismatch;
+        // bit-sliced kernel: strided rows, one row stride for data and parity
+        if (c->bs_ok && !data.table && !par.table && data.stride == par.stride && data.stride >= S) {
+            BsArgs b{};
+            b.data = data.base;
+            b.parity = par.base;
+            b.row_stride = data.stride;
+            b.stripe_stride = stripe_stride;
+            b.S = S;
+            b.k = c->k;
+            b.p = c->p;
+            b.nstripes = nstripes;
+            b.tiles_per_stripe = (int)((S + 4095) / 4096);
+            b.ntiles = b.tiles_per_stripe * nstripes;
+            b.mismatch = mismatch;
+            if (!c->cus) HIP_TRY(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
+            HIP_TRY(launch_encode_bs(mismatch != nullptr, b, std::min(b.ntiles, c->cus), s));
+            return RS_OK;
+        }
         // split kernel: strided rows whose data span fits a 32-bit buffer offset
         const uint64_t span = (uint64_t)(c->k - 1) * data.stride + S;
         if (c->split_ok && !data.table && !par.table && span < (1ull << 32)) {

@@ -118,8 +118,14 @@ __device__ __forceinline__ void ldw_lds(const uint8_t *p, uint32_t (&v)[W]) {
 }
 
 // Verify's mismatch word lives in host-mapped pinned memory (codec.cpp): every
-// writer stores the same 1, so a plain system-scope store suffices.
-__device__ __forceinline__ void flag_mismatch(int *f) { __hip_atomic_store(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+// writer stores the same 1, so a plain system-scope store suffices.  One lane
+// per wave stores (system-scope stores from every lane of every wave of a
+// fully mismatching stripe serialize over the host link).
+__device__ __forceinline__ void flag_mismatch(int *f, bool bad) {
+    const uint64_t m = __ballot(bad);
+    if (m && __lane_id() == (unsigned)(__ffsll((unsigned long long)m) - 1))
+        __hip_atomic_store(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
     return __builtin_amdgcn_perm(s0, s1, sel);
@@ -690,7 +696,7 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
 #pragma unroll
         for (int r = 0; r < M; r++)
             if (r < a.p) bad |= F::diff(acc[r], F::load(rowp<TABLE>(a.parity, r, soff), u));
-        if (bad) flag_mismatch(a.mismatch);
+        flag_mismatch(a.mismatch, bad != 0);
     } else {
 #pragma unroll
         for (int r = 0; r < M; r++)
@@ -956,7 +962,7 @@ __global__ void __launch_bounds__(256, 4) k_encode_split(EncodeArgs a) {
         }
     }
     if constexpr (VERIFY) {
-        if (bad) flag_mismatch(a.mismatch);
+        flag_mismatch(a.mismatch, bad != 0);
     }
 }
 
@@ -1040,7 +1046,7 @@ __global__ void __launch_bounds__(256) k_copy_out(RowSet out, const uint8_t *wor
     const int r = blockIdx.y + r_off;
     Bytes16::Vec v = Bytes16::load(work + (uint64_t)r * S, u);
     if constexpr (VERIFY) {
-        if (Bytes16::diff(v, Bytes16::load(row_ptr(out, r), u))) flag_mismatch(mismatch);
+        flag_mismatch(mismatch, Bytes16::diff(v, Bytes16::load(row_ptr(out, r), u)) != 0);
     } else {
         Bytes16::store(row_ptr(out, r), u, v);
     }
@@ -1344,7 +1350,7 @@ __global__ void __launch_bounds__(256) k_enc_lds(EncodeArgs a) {
         else F::store(prow, u, v);
     }
     if constexpr (VERIFY) {
-        if (bad) flag_mismatch(a.mismatch);
+        flag_mismatch(a.mismatch, bad != 0);
     }
 }
 

@@ -81,4 +81,17 @@ hipError_t launch_rec_lds(int bits, int logn, const RecArgs &a, hipStream_t s);
 // Encode (or verify) for 2 <= logm <= 8, twiddles as for launch_encode_reg.
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 
+
+// ---- Bit-sliced encode (csrc/bitslice.hip): GF(2^16), m = 32, geometries
+// compiled in at build time (Makefile BS_CONFIGS).  Strided rows only.
+struct BsArgs {
+    const uint8_t *data;    // stripe 0, data row 0
+    uint8_t *parity;        // stripe 0, parity row 0
+    uint64_t row_stride, stripe_stride, S;
+    int k, p, nstripes, tiles_per_stripe, ntiles;  // tile = 4 KB of every row of one stripe
+    int *mismatch;          // verify
+};
+bool encode_bs_available(int k, int p);
+hipError_t launch_encode_bs(bool verify, const BsArgs &a, int grid, hipStream_t s);
+
 }  // namespace rs

@@ -19,18 +19,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def short(name: str) -> str:
     if "rs::" not in name:
         return re.split(r"[<(]", name.replace("void ", ""), 1)[0][:80]
-    return name.replace("void ", "").replace("rs::(anonymous namespace)::", "").replace("(rs::EncodeArgs)", "")
+    name = name.replace("void ", "").replace("rs::(anonymous namespace)::", "")
+    return re.sub(r"\(rs::\w+\)$", "", name)
 
 
 def path_of(name: str):
-    """k_encode_reg<F16<W>, LOGM, VERIFY, TABLE> -> the engine's path name (codec.cpp)."""
+    """Kernel symbol -> the engine's path name (codec.cpp plan_encode_host)."""
+    def v(flag):
+        return "-verify" if flag == "true" else ""
+    m = re.search(r"k_encode_bs<.*BsTw<\d+, \d+>, (false|true)>", name)
+    if m:
+        return "bs16-m32" + v(m.group(1))
     m = re.search(r"k_encode_split<(\d+), (false|true)>", name)
     if m:
-        return f"split16-m{1 << int(m.group(1))}" + ("-verify" if m.group(2) == "true" else "")
+        return f"split16-m{1 << int(m.group(1))}" + v(m.group(2))
+    m = re.search(r"k_enc_lds<rs::\(anonymous namespace\)::F(16|8)<\d+>, (\d+), (false|true)>", name)
+    if m:
+        return f"lds-m{1 << int(m.group(2))}" + v(m.group(3))
     m = re.search(r"k_encode_reg<rs::\(anonymous namespace\)::F(16|8)<\d+>, (\d+), (false|true)", name)
-    if not m:
-        return None
-    return f"reg{m.group(1)}-m{1 << int(m.group(2))}" + ("-verify" if m.group(3) == "true" else "")
+    if m:
+        return f"reg{m.group(1)}-m{1 << int(m.group(2))}" + v(m.group(3))
+    return None
 
 
 def main():
@@ -78,7 +87,7 @@ def main():
                       "round": tag}
         lines.append(f"{p}: FETCH_SIZE {fetch/1e6:.2f} MB (x2 = {2*fetch/1e6:.2f}), WRITE_SIZE {write/1e6:.2f} MB, "
                      f"HBM {hbm/1e6:.2f} MB/launch over {len(fk)} launches")
-    kern = [r for r in rows if "k_encode" in r["Name"]]
+    kern = [r for r in rows if "k_enc" in r["Name"]]
     for r in kern:
         lines.append(f"trace {short(r['Name'])}: calls {r['Calls']} avg {float(r['AverageNs'])/1e3:.2f} us "
                      f"min {float(r['MinNs'])/1e3:.2f} max {float(r['MaxNs'])/1e3:.2f}")
