@@ -1,8 +1,9 @@
 """Headline benchmark: device-resident GF(2^16) encode, 128 data + 32 parity x 1 MiB
-shards (BASELINE.json configs[2] / C3), one stripe per rank per step.
+shards (BASELINE.json configs[2] / C3), --stripes stripes (default 8) per rank per step.
 
-A step is one encode of one synthetic stripe already resident in HBM (one
-kernel launch).  Multi-GPU: one process per GPU, each rank encodes its own
+A step is one encode of B synthetic C3 stripes already resident in HBM, all in
+one kernel launch (rs_encode_dev_batch; the stripes are independent objects,
+as a storage server encodes many at once).  Multi-GPU: one process per GPU, each rank encodes its own
 stripe (independent objects, no collective on the data path) -> weak scaling;
 value = data bytes encoded by all ranks / max-over-ranks wall time.
 
@@ -144,7 +145,8 @@ def main():
             "dtype": "u8 (GF(2^16) symbols)",
             "data": "synthetic (uniform random bytes, torch.randint seed 0x5EED+rank)",
             "config": {
-                "workload": "GF(2^16) Leopard encode, 128 data + 32 parity shards x 1 MiB, 1 stripe per rank per step",
+                "workload": f"GF(2^16) Leopard encode, 128 data + 32 parity shards x 1 MiB, {B} stripes per rank per step (one launch)",
+                "stripes_per_step": B,
                 "data_shards": K,
                 "parity_shards": P,
                 "shard_bytes": S,

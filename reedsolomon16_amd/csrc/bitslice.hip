@@ -61,6 +61,9 @@ __device__ __forceinline__ void bs_xchg(uint32_t &a, uint32_t &b, int s, uint32_
 // dwords 8-15: high bytes) <-> 16 bit-planes (plane b bit 8j+w = bit b of symbol
 // 4w+j; planes 8-15 from the high bytes).  An involution.
 __device__ __forceinline__ void bs_transpose(Planes &w) {
+#ifdef RS_BS_ABL_NOTRANS
+    return;
+#endif
 #pragma unroll
     for (int h = 0; h < 16; h += 8)
 #pragma unroll
@@ -83,6 +86,9 @@ __device__ __forceinline__ void xor16(Planes &y, const Planes &x) {
 // matrix row selects.
 template <class TW, int C, int SLOT>
 __device__ __forceinline__ void bs_mul_add(Planes &x, const Planes &y) {
+#ifdef RS_BS_ABL_NOMUL  // ablation (performance experiments only)
+    return;
+#endif
 #pragma unroll
     for (int i = 0; i < 16; i++) {
         const uint32_t r = C < 0 ? TW::fft[SLOT][i] : TW::ifft[C < 0 ? 0 : C][SLOT][i];
@@ -154,12 +160,20 @@ __device__ __forceinline__ uint32_t row_addr(uint32_t lbase, int row) {
     return b + (uint32_t)row * 4096u;
 }
 __device__ __forceinline__ void lds_put(uint32_t lbase, int row, const Planes &v) {
+#ifdef RS_BS_ABL_NOLDS
+    return;
+#endif
     const uint32_t ra = row_addr(lbase, row);
 #pragma unroll
     for (int q = 0; q < 4; q++)
         *(lds_u4 *)(uintptr_t)(ra + q * 1024) = u32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
 }
 __device__ __forceinline__ void lds_get(uint32_t lbase, int row, Planes &v) {
+#ifdef RS_BS_ABL_NOLDS
+#pragma unroll
+    for (int q = 0; q < 16; q++) asm volatile("" : "+v"(v[q]));
+    return;
+#endif
     const uint32_t ra = row_addr(lbase, row);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -170,6 +184,12 @@ __device__ __forceinline__ void lds_get(uint32_t lbase, int row, Planes &v) {
         v[4 * q + 3] = x[3];
     }
 }
+
+// Workgroup barrier for the LDS image only.  __syncthreads() is also a
+// release/acquire fence, which waits for every outstanding global load
+// (vmcnt(0)) and so would drain the next chunk's prefetch at the first
+// barrier of every chunk; this waits for LDS traffic alone.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 typedef __attribute__((address_space(1))) const u32x4 gc_u4;
 typedef __attribute__((address_space(1))) u32x4 g_u4;
@@ -189,7 +209,11 @@ struct BsEncoder {
         const int tps = a.tiles_per_stripe;
         const int stripe = tile / tps, ct = tile - stripe * tps;
         const uint64_t col = (uint64_t)ct * 4096 + (uint64_t)lane * 64;
+#ifdef RS_BS_ABL_NOLOAD
+        const bool ok = false;
+#else
         const bool ok = tile < a.ntiles && col < a.S;
+#endif
         const uint8_t *base = a.data + (uint64_t)stripe * a.stripe_stride + col;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -198,7 +222,11 @@ struct BsEncoder {
                 gc_u4 *p = (gc_u4 *)(base + (uint64_t)row * a.row_stride);
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
+#ifdef RS_BS_ABL_COALESCED  // same bytes, lane-contiguous 16-byte pieces (wrong layout)
+                    const u32x4 x = *(gc_u4 *)(base - (uint64_t)lane * 64 + (uint64_t)row * a.row_stride + q * 1024 + lane * 16);
+#else
                     const u32x4 x = p[q];
+#endif
                     St[i][4 * q] = x[0];
                     St[i][4 * q + 1] = x[1];
                     St[i][4 * q + 2] = x[2];
@@ -220,17 +248,24 @@ struct BsEncoder {
             for (int q = 0; q < 16; q++) R[i][q] = St[i][q];
             bs_transpose(R[i]);
         }
-        // the staged rows are dead before the next chunk's loads reuse their registers
+        // The staged rows are consumed before the next chunk's loads are
+        // issued: the memory clobber keeps IR passes from sinking the
+        // transposes below those loads (which made the wait for the current
+        // rows also wait for the prefetch, serializing HBM and compute).
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) asm volatile("" : "+v"(R[i][q])::"memory");
         __builtin_amdgcn_sched_barrier(0);
         if (C + 1 < NCH) stage(tile, C + 1);
         else stage(tile + (int)gridDim.x, 0);
         __builtin_amdgcn_sched_barrier(0);
         // pass 1: rows 4w + i, radix-4 at dist 1 (group w, slots 3w..3w+2)
         dispatch<8>(w, [&](auto W) { bs_ifft4<TW, C, 3 * decltype(W)::value>(R); });
-        __syncthreads();  // previous readers of the image are done
+        lds_barrier();  // previous readers of the image are done
 #pragma unroll
         for (int i = 0; i < 4; i++) lds_put(lbase, 4 * w + i, R[i]);
-        __syncthreads();
+        lds_barrier();
         // pass 2: rows 16h + j + 4i, radix-4 at dist 4 (group h, slots 24 + 3h ..)
         const int h = w >> 2, j = w & 3;
 #pragma unroll
@@ -238,7 +273,7 @@ struct BsEncoder {
         dispatch<2>(h, [&](auto H) { bs_ifft4<TW, C, 24 + 3 * decltype(H)::value>(R); });
 #pragma unroll
         for (int i = 0; i < 4; i++) lds_put(lbase, 16 * h + j + 4 * i, R[i]);
-        __syncthreads();
+        lds_barrier();
         // pass 3: rows w + 8i, radix-2 at dist 16 (slot 30): pairs (w, w+16), (w+8, w+24)
 #pragma unroll
         for (int i = 0; i < 4; i++) lds_get(lbase, w + 8 * i, R[i]);
@@ -281,10 +316,10 @@ struct BsEncoder {
                 for (int q = 0; q < 16; q++) R[i][q] = A[i][q];
             lds_get(lbase, 32 + w, R[3]);
             bs_fft4<TW, 0>(R);
-            __syncthreads();
+            lds_barrier();
 #pragma unroll
             for (int i = 0; i < 4; i++) lds_put(lbase, w + 8 * i, R[i]);
-            __syncthreads();
+            lds_barrier();
             // pass B: rows 8g + j + 2i (dist 4 then 2; group g, slots 3 + 3g ..)
             const int g = w >> 1, j = w & 1;
 #pragma unroll
@@ -292,7 +327,7 @@ struct BsEncoder {
             dispatch<4>(g, [&](auto G) { bs_fft4<TW, 3 + 3 * decltype(G)::value>(R); });
 #pragma unroll
             for (int i = 0; i < 4; i++) lds_put(lbase, 8 * g + j + 2 * i, R[i]);
-            __syncthreads();
+            lds_barrier();
             // pass C: rows 4w + i, radix-2 at dist 1 (slots 15 + 2w, 16 + 2w)
 #pragma unroll
             for (int i = 0; i < 4; i++) lds_get(lbase, 4 * w + i, R[i]);
@@ -313,15 +348,24 @@ struct BsEncoder {
                     const int row = 4 * w + i;
                     if (row >= a.p) continue;
                     bs_transpose(R[i]);
+#ifdef RS_BS_ABL_COALESCED
+                    g_u4 *q = (g_u4 *)(base - (uint64_t)lane * 64 + (uint64_t)row * a.row_stride + lane * 16);
+#else
                     g_u4 *q = (g_u4 *)(base + (uint64_t)row * a.row_stride);
+#endif
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
+#ifdef RS_BS_ABL_COALESCED
+                        const int kq = k * 64;  // 1 KB apart
+#else
+                        const int kq = k;
+#endif
                         const u32x4 v = u32x4{R[i][4 * k], R[i][4 * k + 1], R[i][4 * k + 2], R[i][4 * k + 3]};
                         if constexpr (VERIFY) {
-                            const u32x4 o = q[k];
+                            const u32x4 o = q[kq];
                             bad |= (o[0] ^ v[0]) | (o[1] ^ v[1]) | (o[2] ^ v[2]) | (o[3] ^ v[3]);
                         } else {
-                            q[k] = v;
+                            q[kq] = v;
                         }
                     }
                 }

@@ -199,10 +199,10 @@ int upload_split(rs_codec *c) {
     return RS_OK;
 }
 
-// The bit-sliced kernel is opt-in (RS_BS=1) until it is parity-green on the GPU.
+// RS_BS=0 disables the bit-sliced kernel (A/B experiments only).
 bool bs_enabled() {
     const char *e = getenv("RS_BS");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 
 // RS_NO_SPLIT=1 disables the split kernel (A/B experiments only).

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Bit-sliced kernel ablations (performance experiments only): one library per
+# variant in build/ablate_bs/<name>/, 128+32 geometry only.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+set -e
+HIPCC=/opt/rocm/bin/hipcc
+SRC=reedsolomon16_amd/csrc
+B=reedsolomon16_amd/build
+OUT=build/ablate_bs
+rm -rf $OUT; mkdir -p $OUT/common
+$B/gen_bs_tables $OUT/common/bs_tables.h 128:32
+for v in ${VARIANTS:-base: nomul:-DRS_BS_ABL_NOMUL nolds:-DRS_BS_ABL_NOLDS noload:-DRS_BS_ABL_NOLOAD notrans:-DRS_BS_ABL_NOTRANS}; do
+  name=${v%%:*}; flags=${v#*:}; flags=${flags//,/ }
+  mkdir -p $OUT/$name
+  $HIPCC --offload-arch=gfx950 -O3 -std=c++17 -fPIC $flags -I$OUT/common -c $SRC/bitslice.hip -o $OUT/$name/bitslice.o &
+done
+wait
+for d in $OUT/*/; do
+  [ "$(basename $d)" = common ] && continue
+  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $d/librs_mi355x.so $B/kernels.o $d/bitslice.o $B/gf_host.o $B/codec.o
+done

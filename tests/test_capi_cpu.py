@@ -128,7 +128,8 @@ def test_constructor_errors():
     c = rs.New(10, 4)
     assert c.field_bits == 8 and c.total_shards() == 14 and c.shard_size_multiple() == 64
     assert rs.New(200, 100).field_bits == 16
-    assert rs.New16(128, 32).encode_path == "split16-m32"
+    assert rs.New16(128, 32).encode_path == "bs16-m32"  # bit-sliced kernel compiled in for 128+32
+    assert rs.New16(130, 32).encode_path == "split16-m32"
     assert rs.New16(10, 1).encode_path == "reg16-m1"
     assert rs.New16(1024, 256).encode_path == "lds-m256"
     assert rs.New16(1024, 300).encode_path == "multipass"
