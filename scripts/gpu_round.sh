@@ -9,6 +9,8 @@ OUT=gpurun_out/round
 rm -rf $OUT
 mkdir -p $OUT
 BARGS="${BENCH_ARGS:-}"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' > $OUT/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -2 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py $BARGS > $OUT/bench.json 2> $OUT/bench.err
