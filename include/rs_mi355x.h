@@ -131,6 +131,13 @@ int rs_debug_field_tables(int field_bits, uint16_t *log_out, uint16_t *exp_out, 
 /* Byte-permute twiddle image of "multiply by exp(log_m)" (rs_debug_twiddle_dwords() dwords). */
 int rs_debug_twiddle(int field_bits, uint32_t log_m, uint32_t *out);
 int rs_debug_twiddle_dwords(int field_bits);
+/* GF(2^8)-subfield coordinates of GF(2^16) (x0, x1) = (lo ^ D(hi), hi): 0 when the
+ * engine verified that a subfield product acts as one 8x8 map on both bytes. */
+int rs_debug_sub_check(void);
+/* 8-dword subfield table of "multiply by exp(log_m)"; -1 if exp(log_m) is not in GF(2^8). */
+int rs_debug_sub_twiddle(uint32_t log_m, uint32_t *out);
+/* Symbol <-> subfield coordinates (an involution). */
+uint32_t rs_debug_sub_swap(uint32_t x);
 /* Error locators for an erasure pattern (leopard16.go:433-470); out has 2^field_bits entries.
  * Returns RS_ERR_PANIC where the reference panics. */
 int rs_debug_error_locators(int field_bits, int data_shards, int parity_shards, const uint8_t *erased,

@@ -54,6 +54,10 @@ def lib() -> C.CDLL:
     L.rs_debug_error_locators.argtypes = [i32, i32, i32, vp, vp]
     L.rs_debug_split_check.argtypes = [i32, C.c_uint32]
     L.rs_debug_split_emulate.argtypes = [vp, vp, vp, sz]
+    L.rs_debug_sub_check.argtypes = []
+    L.rs_debug_sub_twiddle.argtypes = [C.c_uint32, vp]
+    L.rs_debug_sub_swap.argtypes = [C.c_uint32]
+    L.rs_debug_sub_swap.restype = C.c_uint32
     _lib = L
     return L
 

@@ -95,6 +95,7 @@ struct rs_codec {
 
     // decode plan (built on first reconstruct)
     bool dec_built = false, dec_ok = false;
+    bool dec_sub = false;  // LDS reconstruct runs its transforms in subfield coordinates
     int n = 0, logn = 0;
     DevBuf<uint32_t> dtw_ifft, dtw_fft;
 
@@ -205,6 +206,12 @@ bool bs_enabled() {
     return !(e && e[0] == '0');
 }
 
+// RS_NO_SUB=1 disables subfield-coordinate transforms (A/B experiments only).
+bool sub_enabled() {
+    const char *e = getenv("RS_NO_SUB");
+    return !(e && e[0] == '1');
+}
+
 // RS_NO_SPLIT=1 disables the split kernel (A/B experiments only).
 bool split_enabled() {
     const char *e = getenv("RS_NO_SPLIT");
@@ -252,6 +259,21 @@ int build_decode_plan(rs_codec *c) {
     if (!c->dec_ok) return RS_OK;
     c->n = ceil_pow2(c->m + c->k);
     c->logn = ilog2(c->n);
+    // n <= 256: every decoder twiddle is fftSkew[< 255], an element of GF(2^8)
+    bool sub = c->bits == 16 && c->logn <= kMaxLdsLogN && sub_enabled() && sub_coords().ok;
+    for (uint32_t l : il) sub = sub && in_subfield(*c->F, l);
+    for (uint32_t l : fl) sub = sub && in_subfield(*c->F, l);
+    if (sub) {
+        std::vector<uint32_t> hi(std::max<size_t>(il.size(), 1) * kTwDwords8, 0), hf(std::max<size_t>(fl.size(), 1) * kTwDwords8, 0);
+        for (size_t i = 0; i < il.size(); i++) make_sub_twiddle(*c->F, il[i], hi.data() + i * kTwDwords8);
+        for (size_t i = 0; i < fl.size(); i++) make_sub_twiddle(*c->F, fl[i], hf.data() + i * kTwDwords8);
+        HIP_TRY(c->dtw_ifft.ensure(hi.size()));
+        HIP_TRY(c->dtw_fft.ensure(hf.size()));
+        HIP_TRY(hipMemcpy(c->dtw_ifft.p, hi.data(), hi.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->dtw_fft.p, hf.data(), hf.size() * 4, hipMemcpyHostToDevice));
+        c->dec_sub = true;
+        return RS_OK;
+    }
     int e = upload_twiddles(c, il, c->dtw_ifft);
     if (e) return e;
     return upload_twiddles(c, fl, c->dtw_fft);
@@ -431,8 +453,15 @@ int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool reco
     for (int i = 0; i < k; i++)
         if (present[i]) pl.src_shard[m + i] = i;
     pl.tw_in.assign((size_t)n * c->twd, 0);
-    for (int r = 0; r < m + k; r++)
-        if (pl.src_shard[r] >= 0) make_twiddle(*c->F, el[r], pl.tw_in.data() + (size_t)r * c->twd);
+    const Field &F = *c->F;
+    const SubCoords &sc = sub_coords();
+    for (int r = 0; r < m + k; r++) {
+        if (pl.src_shard[r] < 0) continue;
+        if (c->dec_sub)  // x -> subfield coordinates of x * errLocs[r]
+            make_linear_image([&](uint32_t x) { return sc.to_sub(F.mul_log(x, el[r])); }, pl.tw_in.data() + (size_t)r * c->twd);
+        else
+            make_twiddle(F, el[r], pl.tw_in.data() + (size_t)r * c->twd);
+    }
     pl.dst_shard.clear();
     pl.pos.clear();
     const int end = recover_all ? total : k;
@@ -442,8 +471,13 @@ int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool reco
         pl.pos.push_back(i >= k ? i - k : i + m);
     }
     pl.tw_out.assign(std::max<size_t>(pl.dst_shard.size(), 1) * c->twd, 0);
-    for (size_t j = 0; j < pl.dst_shard.size(); j++)
-        make_twiddle(*c->F, (c->F->mod - el[pl.pos[j]]) & c->F->mod, pl.tw_out.data() + j * c->twd);
+    for (size_t j = 0; j < pl.dst_shard.size(); j++) {
+        const uint32_t lg = (F.mod - el[pl.pos[j]]) & F.mod;
+        if (c->dec_sub)  // subfield coordinates y -> symbol(y) * exp(lg)
+            make_linear_image([&](uint32_t y) { return F.mul_log(sc.to_sub(y), lg); }, pl.tw_out.data() + j * c->twd);
+        else
+            make_twiddle(F, lg, pl.tw_out.data() + j * c->twd);
+    }
     return RS_OK;
 }
 
@@ -489,7 +523,7 @@ int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipS
         ra.S = S;
         ra.mtrunc = c->m + c->k;
         ra.nd = nd;
-        HIP_TRY(launch_rec_lds(c->bits, c->logn, ra, s));
+        HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
         return RS_OK;
     }
     HIP_TRY(c->work.ensure((size_t)n * S));
@@ -1051,6 +1085,17 @@ int rs_debug_field_tables(int bits, uint16_t *log_out, uint16_t *exp_out, uint16
 }
 
 int rs_debug_twiddle_dwords(int bits) { return (bits == 8 || bits == 16) ? tw_dwords(bits) : 0; }
+
+int rs_debug_sub_check(void) { return sub_coords().ok ? 0 : -1; }
+
+int rs_debug_sub_twiddle(uint32_t log_m, uint32_t *out) {
+    const Field &F = field(16);
+    if (!out || log_m > F.mod || !in_subfield(F, log_m)) return -1;
+    make_sub_twiddle(F, log_m, out);
+    return 0;
+}
+
+uint32_t rs_debug_sub_swap(uint32_t x) { return sub_coords().to_sub(x & 0xFFFF); }
 
 int rs_debug_twiddle(int bits, uint32_t log_m, uint32_t *out) {
     if ((bits != 8 && bits != 16) || !out) return RS_ERR_INVALID_ARG;

@@ -143,6 +143,51 @@ void make_twiddle(const Field &F, uint32_t log_m, uint32_t *out, bool zero_if_mo
     while (d < n) out[d++] = 0;
 }
 
+const SubCoords &sub_coords() {
+    static std::once_flag once;
+    static SubCoords sc;
+    std::call_once(once, [] {
+        const Field &F = field(16);
+        const uint32_t lb8 = F.log[256];
+        for (int i = 0; i < 8; i++) {
+            bool found = false;
+            for (uint32_t c = 1; c < 256 && !found; c++) {
+                const uint32_t dd = F.mul_log(c, lb8) ^ (1u << (8 + i));  // 1<<(8+i) = dd + beta8*c
+                if (dd < 256) {
+                    sc.d[i] = (uint8_t)dd;
+                    found = true;
+                }
+            }
+            if (!found) return;
+        }
+        // multiply-by-t in coordinates == (t*x0, t*x1), checked on the basis for every subfield t
+        for (uint32_t t = 1; t < 256; t++) {
+            const uint32_t lt = F.log[t];
+            for (int j = 0; j < 16; j++) {
+                const uint32_t got = sc.to_sub(F.mul_log(sc.to_sub(1u << j), lt));
+                const uint32_t want = j < 8 ? F.mul_log(1u << j, lt) : F.mul_log(1u << (j - 8), lt) << 8;
+                if (got != want) return;
+            }
+        }
+        sc.ok = true;
+    });
+    return sc;
+}
+
+void make_sub_twiddle(const Field &F, uint32_t log_m, uint32_t *out) {
+    static const int off[3] = {0, 3, 6}, wid[3] = {3, 3, 2};
+    int d = 0;
+    for (int g = 0; g < 3; g++) {
+        uint8_t e[8] = {0};
+        if (log_m != F.mod)
+            for (int x = 0; x < (1 << wid[g]); x++) e[x] = (uint8_t)F.mul_log((uint32_t)x << off[g], log_m);
+        out[d++] = e[0] | (e[1] << 8) | (e[2] << 16) | ((uint32_t)e[3] << 24);
+        if (wid[g] == 3) out[d++] = e[4] | (e[5] << 8) | (e[6] << 16) | ((uint32_t)e[7] << 24);
+    }
+    out[d++] = log_m;
+    while (d < kTwDwords8) out[d++] = 0;
+}
+
 std::vector<PassInfo> ifft_passes(int logm) {
     std::vector<PassInfo> v;
     const int M = 1 << logm;

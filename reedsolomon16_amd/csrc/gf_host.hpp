@@ -47,6 +47,48 @@ const Field &field(int bits);  // built once, thread-safe
 void make_twiddle(const Field &F, uint32_t log_m, uint32_t *out, bool zero_if_mod = false);
 inline int tw_dwords(int bits) { return bits == 16 ? kTwDwords16 : kTwDwords8; }
 
+// ---- GF(2^8) inside GF(2^16) ("subfield coordinates").
+// The Cantor-basis integers < 256 (the span of the first 8 basis vectors,
+// leopard16.go:941-946) form the subfield GF(2^8), and every fftSkew entry
+// with index < 255 lies in it (initFFTSkew :986-1031 builds them from
+// 2, 4, ..., 128 by field operations).  Write the element 1 << (8+i) as
+// d_i + beta8 * c_i (beta8 = the element 256, c_i, d_i < 256).  Holding a
+// symbol as (x0, x1) = (lo ^ D(hi), hi), D(h) = XOR of d_i over the set bits
+// of h, a product with a subfield element t is (t*x0, t*x1): one 8x8 GF(2)
+// map on both bytes.  to_sub is an involution (it is its own inverse).
+struct SubCoords {
+    bool ok = false;  // the block structure was verified for every subfield element
+    uint8_t d[8] = {};
+    uint32_t D(uint32_t hi) const {
+        uint32_t r = 0;
+        for (int i = 0; i < 8; i++)
+            if ((hi >> i) & 1) r ^= d[i];
+        return r;
+    }
+    uint32_t to_sub(uint32_t x) const { return x ^ D(x >> 8); }
+};
+const SubCoords &sub_coords();  // GF(2^16); built once, thread-safe
+// log_m is the zero twiddle (== mod) or exp(log_m) lies in the subfield.
+inline bool in_subfield(const Field &F, uint32_t log_m) { return log_m == F.mod || F.exp[log_m] < 256; }
+// GF(2^8)-layout (kTwDwords8) table of "multiply by exp(log_m)" on one byte of
+// subfield coordinates; log_m == mod gives the all-zero table.  log_m at dword 5.
+void make_sub_twiddle(const Field &F, uint32_t log_m, uint32_t *out);
+// GF(2^16)-layout (kTwDwords16) table of an arbitrary GF(2)-linear map f on
+// 16-bit symbols (same group/byte layout as make_twiddle; dword 20 = 0).
+template <class Fn>
+void make_linear_image(Fn f, uint32_t *out) {
+    static const int off[6] = {0, 3, 6, 8, 11, 14}, wid[6] = {3, 3, 2, 3, 3, 2};
+    int d = 0;
+    for (int g = 0; g < 6; g++)
+        for (int o = 0; o < 2; o++) {
+            uint8_t e[8] = {0};
+            for (int x = 0; x < (1 << wid[g]); x++) e[x] = (uint8_t)(f((uint32_t)x << off[g]) >> (8 * o));
+            out[d++] = e[0] | (e[1] << 8) | (e[2] << 16) | ((uint32_t)e[3] << 24);
+            if (wid[g] == 3) out[d++] = e[4] | (e[5] << 8) | (e[6] << 16) | ((uint32_t)e[7] << 24);
+        }
+    while (d < kTwDwords16) out[d++] = 0;
+}
+
 inline int ceil_pow2(int n) { return n <= 1 ? 1 : 1 << (64 - __builtin_clzll((unsigned long long)(n - 1))); }
 inline int ilog2(int n) { return 31 - __builtin_clz((unsigned)n); }
 

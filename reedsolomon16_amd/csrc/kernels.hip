@@ -139,6 +139,7 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 template <int W_>
 struct F16 {
     static constexpr int W = W_;
+    static constexpr bool SYM16 = true;  // 16-bit symbols (lo/hi halves of 64-byte blocks)
     static constexpr int TWD = 24;     // dwords per twiddle table
     static constexpr int TWU = 20;     // dwords used by mul_add
     static constexpr int LOGIDX = 20;  // dword holding log_m
@@ -226,6 +227,7 @@ struct F16 {
 template <int W_>
 struct F8 {
     static constexpr int W = W_;
+    static constexpr bool SYM16 = false;
     static constexpr int TWD = 8;
     static constexpr int TWU = 5;
     static constexpr int LOGIDX = 5;
@@ -276,6 +278,29 @@ struct F8 {
             const uint32_t v = y.b[i];
             const uint32_t a0 = v & 0x07070707u, a1 = (v >> 3) & 0x07070707u, a2 = (v >> 6) & 0x03030303u;
             x.b[i] = xor3(x.b[i] ^ perm(t[1], t[0], a0), perm(t[3], t[2], a1), perm(t[4], t[4], a2));
+        }
+    }
+};
+
+// ---------------------------------------------------------------- GF(2^16) in subfield coordinates
+// Transforms whose twiddles all lie in GF(2^8) (fftSkew indices < 255, e.g. the
+// n = 256 reconstruct of C4) run on symbols held as (x0, x1) = (lo ^ D(hi), hi)
+// (gf_host.hpp SubCoords): a product with a subfield element is the same 8x8
+// map on both bytes, 6 v_perm_b32 per 4 symbols with one GF(2^8)-layout table
+// instead of 12.  Loads/stores are F16's; the coordinate change is folded into
+// the full-field tables that scale the rows in and out.
+template <int W_>
+struct F16S : F16<W_> {
+    static constexpr int TWD = 8, TWU = 5, LOGIDX = 5;
+    typedef typename F16<W_>::Vec Vec;
+    __device__ static void mul_add(Vec &x, const Vec &y, const uint32_t *__restrict__ t) {
+#pragma unroll
+        for (int i = 0; i < W_; i++) {
+            const uint32_t lo = y.l[i], hi = y.h[i];
+            x.l[i] = xor3(x.l[i] ^ perm(t[1], t[0], lo & 0x07070707u), perm(t[3], t[2], (lo >> 3) & 0x07070707u),
+                          perm(t[4], t[4], (lo >> 6) & 0x03030303u));
+            x.h[i] = xor3(x.h[i] ^ perm(t[1], t[0], hi & 0x07070707u), perm(t[3], t[2], (hi >> 3) & 0x07070707u),
+                          perm(t[4], t[4], (hi >> 6) & 0x03030303u));
         }
     }
 };
@@ -1109,7 +1134,7 @@ hipError_t for_y(int total, Fn body) {
 template <class F, int LOGM>
 hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
     uint64_t nunits;
-    if constexpr (F::TWD == 24) nunits = (a.shard_size >> 6) * (8 / F::W);
+    if constexpr (F::SYM16) nunits = (a.shard_size >> 6) * (8 / F::W);
     else nunits = a.shard_size / (4 * F::W);
     dim3 grid((unsigned)((nunits + 255) / 256), (unsigned)a.nstripes);
     const bool table = a.data.table != nullptr || a.parity.table != nullptr;
@@ -1141,7 +1166,7 @@ constexpr int kLdsRow = 144;  // LDS row stride: 36 dwords spreads rows over the
 
 template <class F>
 struct LTile {
-    static constexpr bool W16 = F::TWD == 24;
+    static constexpr bool W16 = F::SYM16;
     static constexpr int UB = W16 ? 8 * F::W : 4 * F::W;  // global bytes per unit
     static constexpr int U = kTileB / UB;                 // units per tile
     typedef typename F::Vec V;
@@ -1253,7 +1278,9 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
 }
 
 // Reconstruct (leopard16.go:432-568) of one stripe, one 128-byte tile per workgroup.
-template <class F, int LOGN>
+// F scales rows in and out (full-field tables); FT runs the transforms (F, or
+// F16S when every transform twiddle lies in GF(2^8)).
+template <class F, class FT, int LOGN>
 __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
@@ -1270,7 +1297,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         L::put(lds, r, u, v);
     }
     __syncthreads();
-    lds_transform<F, true, LOGN>(lds, a.mtrunc, a.tw_ifft);
+    lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft);
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
     {
         V o[K];
@@ -1295,7 +1322,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         }
         __syncthreads();
     }
-    lds_transform<F, false, LOGN>(lds, a.mtrunc, a.tw_fft);
+    lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft);
     // reveal: shard = work[pos] * (modulus - errLocs[pos])
     for (int it = threadIdx.x; it < a.nd * U; it += 256) {
         const int j = it / U, u = it - j * U;
@@ -1354,23 +1381,23 @@ __global__ void __launch_bounds__(256) k_enc_lds(EncodeArgs a) {
     }
 }
 
-template <class F, int LOGN>
+template <class F, class FT, int LOGN>
 hipError_t rec_lds_t(const RecArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)((a.S + kTileB - 1) / kTileB));
-    hipLaunchKernelGGL((k_rec_lds<F, LOGN>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
-template <class F>
+template <class F, class FT = F>
 hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
     switch (logn) {
-        case 1: return rec_lds_t<F, 1>(a, s);
-        case 2: return rec_lds_t<F, 2>(a, s);
-        case 3: return rec_lds_t<F, 3>(a, s);
-        case 4: return rec_lds_t<F, 4>(a, s);
-        case 5: return rec_lds_t<F, 5>(a, s);
-        case 6: return rec_lds_t<F, 6>(a, s);
-        case 7: return rec_lds_t<F, 7>(a, s);
-        case 8: return rec_lds_t<F, 8>(a, s);
+        case 1: return rec_lds_t<F, FT, 1>(a, s);
+        case 2: return rec_lds_t<F, FT, 2>(a, s);
+        case 3: return rec_lds_t<F, FT, 3>(a, s);
+        case 4: return rec_lds_t<F, FT, 4>(a, s);
+        case 5: return rec_lds_t<F, FT, 5>(a, s);
+        case 6: return rec_lds_t<F, FT, 6>(a, s);
+        case 7: return rec_lds_t<F, FT, 7>(a, s);
+        case 8: return rec_lds_t<F, FT, 8>(a, s);
     }
     return hipErrorInvalidValue;
 }
@@ -1540,8 +1567,9 @@ hipError_t launch_reveal(int bits, uint8_t *const *dst, const uint8_t *work, uin
 }
 
 
-hipError_t launch_rec_lds(int bits, int logn, const RecArgs &a, hipStream_t s) {
-    return bits == 16 ? rec_lds_f<F16<4>>(logn, a, s) : rec_lds_f<F8<4>>(logn, a, s);
+hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s) {
+    if (bits != 16) return rec_lds_f<F8<4>>(logn, a, s);
+    return sub ? rec_lds_f<F16<4>, F16S<4>>(logn, a, s) : rec_lds_f<F16<4>>(logn, a, s);
 }
 
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s) {

@@ -77,7 +77,9 @@ struct RecArgs {
     int mtrunc;                 // m + k
     int nd;
 };
-hipError_t launch_rec_lds(int bits, int logn, const RecArgs &a, hipStream_t s);
+// sub: GF(2^16) transforms in subfield coordinates (tw_ifft/tw_fft are
+// kTwDwords8 subfield tables; tw_in/tw_out fold in the coordinate change).
+hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s);
 // Encode (or verify) for 2 <= logm <= 8, twiddles as for launch_encode_reg.
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 

@@ -214,3 +214,40 @@ def test_split_kernel_emulation_matches_oracle(k, p, S):
     out = np.zeros((p, S), np.uint8)
     assert rs.lib().rs_debug_split_emulate(c._h, data.ctypes.data, out.ctypes.data, S) == 0
     assert np.array_equal(out, ref)
+
+
+def test_subfield_coordinates():
+    """GF(2^8) inside GF(2^16): products of Cantor-basis integers < 256 stay
+    below 256, every fftSkew entry below index 255 is such an element, and in
+    the engine's coordinates (lo ^ D(hi), hi) the 8-dword subfield table
+    (emulated v_perm_b32 on both bytes) multiplies exactly like the field."""
+    F = lnp.field(16)
+    a = np.arange(1, 256)
+    for b in range(1, 256):
+        assert (F.mul_log(a, int(F._log[b])) < 256).all()
+    sk = F._skew[:255]
+    assert ((sk == 65535) | (F._exp[sk] < 256)).all()
+    L = rs.lib()
+    assert L.rs_debug_sub_check() == 0
+    rng = np.random.default_rng(9)
+    x = rng.integers(0, 65536, 512).astype(np.int64)
+    y = np.array([L.rs_debug_sub_swap(int(v)) for v in x], np.int64)
+    assert np.array_equal(np.array([L.rs_debug_sub_swap(int(v)) for v in y], np.int64), x)
+    m7, m3 = np.uint32(0x07070707), np.uint32(0x03030303)
+
+    def sub_mul(t, bytes_):
+        d = np.ascontiguousarray(bytes_.astype(np.uint8)).view(np.uint32)
+        p = vperm(t[1], t[0], d & m7) ^ vperm(t[3], t[2], (d >> np.uint32(3)) & m7) ^ \
+            vperm(t[4], t[4], (d >> np.uint32(6)) & m3)
+        return p.view(np.uint8).astype(np.int64)
+
+    t = np.zeros(8, np.uint32)
+    for e in (1, 2, 3, 77, 200, 255):
+        log_m = int(F._log[e])
+        assert L.rs_debug_sub_twiddle(log_m, t.ctypes.data) == 0
+        tt = [np.uint32(v) for v in t]
+        z = sub_mul(tt, y & 0xFF) | (sub_mul(tt, y >> 8) << 8)
+        back = np.array([L.rs_debug_sub_swap(int(v)) for v in z], np.int64)
+        assert np.array_equal(back, F.mul_log(x, log_m)), e
+    assert L.rs_debug_sub_twiddle(65535, t.ctypes.data) == 0 and not t[:5].any()
+    assert L.rs_debug_sub_twiddle(int(F._log[300]), t.ctypes.data) == -1
