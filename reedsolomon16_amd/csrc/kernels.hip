@@ -1213,9 +1213,10 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
     constexpr int U = L::U;
     if (radix == 4) {
         const int items = groups_active * dist * U;
+        const int ld = __builtin_ctz((unsigned)dist);  // dist is a power of two: no integer division
         for (int it = threadIdx.x; it < items; it += 256) {
             const int q = it / U, u = it - q * U;
-            const int g = q / dist, j = q - g * dist;
+            const int g = q >> ld, j = q & (dist - 1);
             const int i = g * 4 * dist + j;
             const uint32_t *t = tw + (uint64_t)g * 3 * F::TWD;
             V x0 = L::get(lds, i, u), x1 = L::get(lds, i + dist, u), x2 = L::get(lds, i + 2 * dist, u),
