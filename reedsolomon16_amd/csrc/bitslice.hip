@@ -371,10 +371,10 @@ struct BsEncoder {
                 }
             }
             if constexpr (VERIFY) {
-                // one system-scope store per wave, not per lane (the flag word is host-mapped)
+                // one store per wave, not per lane
                 const uint64_t m = __ballot(bad != 0);
                 if (m && lane == __ffsll((unsigned long long)m) - 1)
-                    __hip_atomic_store(a.mismatch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(a.mismatch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }

@@ -103,7 +103,7 @@ struct rs_codec {
     DevBuf<uint8_t> work;
     DevBuf<uint8_t *> rows;         // row-pointer table (non-strided inputs)
     std::vector<uint8_t *> rows_host;
-    int *hflag = nullptr, *dflag = nullptr;  // verify mismatch word: host-mapped pinned (host view, device view)
+    int *hflag = nullptr, *dflag = nullptr;  // verify mismatch word: device word + pinned host readback
     DevBuf<const uint8_t *> rc_src;
     DevBuf<uint8_t *> rc_dst;
     DevBuf<uint32_t> rc_tw_in, rc_tw_out;
@@ -126,6 +126,7 @@ struct rs_codec {
         tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); dtw_ifft.release(); dtw_fft.release();
         work.release(); rows.release();
         if (hflag) (void)hipHostFree(hflag);
+        if (dflag) (void)hipFree(dflag);
         rc_src.release(); rc_dst.release(); rc_tw_in.release(); rc_tw_out.release(); rc_pos.release();
         if (s_in) (void)hipStreamSynchronize(s_in);
         if (s_out) (void)hipStreamSynchronize(s_out);
@@ -234,8 +235,8 @@ int ensure_device(rs_codec *c) {
     if (c->dev_ready) return RS_OK;
     if (!c->stream) HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     if (!c->hflag) {
-        HIP_TRY(hipHostMalloc((void **)&c->hflag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
-        HIP_TRY(hipHostGetDevicePointer((void **)&c->dflag, c->hflag, 0));
+        HIP_TRY(hipHostMalloc((void **)&c->hflag, sizeof(int), hipHostMallocDefault));
+        HIP_TRY(hipMalloc((void **)&c->dflag, sizeof(int)));
     }
     if (c->enc_ok) {
         int e = upload_twiddles(c, c->enc_ifft_logs, c->tw_ifft);
@@ -665,7 +666,7 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
         e = upload_reconstruct(c, pl, d, src_h, dst_h, sc);
         if (e) return e;
     }
-    if (op == HostOp::Verify) *(volatile int *)c->hflag = 0;  // no verify is in flight: calls are serialized and synchronous
+    if (op == HostOp::Verify) HIP_TRY(hipMemsetAsync(c->dflag, 0, sizeof(int), sc));
     // copies in must not start before this call's setup on the compute stream
     HIP_TRY(hipEventRecord(c->ev_k[0], sc));
     HIP_TRY(hipStreamWaitEvent(c->s_in, c->ev_k[0], 0));
@@ -696,6 +697,7 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
             HIP_TRY(hipEventRecord(c->ev_free[b], sc));
         }
     }
+    if (op == HostOp::Verify) HIP_TRY(hipMemcpyAsync(c->hflag, c->dflag, sizeof(int), hipMemcpyDeviceToHost, sc));
     HIP_TRY(hipStreamSynchronize(c->s_in));
     HIP_TRY(hipStreamSynchronize(sc));
     HIP_TRY(hipStreamSynchronize(c->s_out));
@@ -941,9 +943,10 @@ int rs_verify_dev(rs_codec *c, uint8_t *const *d, size_t S, int *ok, void *strea
     RowSet data, par;
     int e = make_rowsets(c, d, s, data, par);
     if (e) return e;
-    *(volatile int *)c->hflag = 0;  // the previous verify has completed (synchronous calls under the mutex)
+    HIP_TRY(hipMemsetAsync(c->dflag, 0, sizeof(int), s));
     e = encode_device(c, data, par, S, 0, 1, c->dflag, s);
     if (e) return e;
+    HIP_TRY(hipMemcpyAsync(c->hflag, c->dflag, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     *ok = *(volatile int *)c->hflag == 0;
     return RS_OK;
