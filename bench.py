@@ -1,5 +1,5 @@
 """Headline benchmark: device-resident GF(2^16) encode, 128 data + 32 parity x 1 MiB
-shards (BASELINE.json configs[2] / C3), --stripes stripes (default 8) per rank per step.
+shards (BASELINE.json configs[2] / C3), --stripes stripes (default 16) per rank per step.
 
 A step is one encode of B synthetic C3 stripes already resident in HBM, all in
 one kernel launch (rs_encode_dev_batch; the stripes are independent objects,
@@ -69,7 +69,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--stripes", type=int, default=8,
+    ap.add_argument("--stripes", type=int, default=16,
                     help="stripes encoded per step (one launch); each is 128+32 x 1 MiB")
     args = ap.parse_args()
 
