@@ -84,11 +84,43 @@ __device__ __forceinline__ void xor16(Planes &y, const Planes &x) {
 // x ^= y * twiddle (C >= 0: chunk C's IFFT slot; C < 0: FFT slot).
 // Each output plane is a chain of 3-input XORs over the input planes its
 // matrix row selects.
+// out ^= XOR of y[B + j] over the set bits j of mask (3-input XOR pairs).
+__device__ __forceinline__ void xor_rows(uint32_t &out, const Planes &y, int B, uint32_t mask, int nbits) {
+    int pend = -1;
+#pragma unroll
+    for (int j = 0; j < nbits; j++) {
+        if ((mask >> j) & 1) {
+            if (pend < 0) {
+                pend = j;
+            } else {
+                ixor3(out, y[B + pend], y[B + j]);
+                pend = -1;
+            }
+        }
+    }
+    if (pend >= 0) ixor(out, y[B + pend]);
+}
+// Subfield coordinates (gf_host.hpp SubCoords): planes 0-7 ^= D(planes 8-15).
+// An involution; applied after the load transpose and before the store one.
+template <class TW>
+__device__ __forceinline__ void bs_psi(Planes &w) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) xor_rows(w[r], w, 8, TW::dmat[r], 8);
+}
 template <class TW, int C, int SLOT>
 __device__ __forceinline__ void bs_mul_add(Planes &x, const Planes &y) {
 #ifdef RS_BS_ABL_NOMUL  // ablation (performance experiments only)
     return;
 #endif
+    if constexpr (TW::SUB) {
+        // one 8x8 network per byte half
+#pragma unroll
+        for (int h = 0; h < 16; h += 8)
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                xor_rows(x[h + i], y, h, C < 0 ? TW::fft8[SLOT][i] : TW::ifft8[C < 0 ? 0 : C][SLOT][i], 8);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 16; i++) {
         const uint32_t r = C < 0 ? TW::fft[SLOT][i] : TW::ifft[C < 0 ? 0 : C][SLOT][i];
@@ -247,6 +279,7 @@ struct BsEncoder {
 #pragma unroll
             for (int q = 0; q < 16; q++) R[i][q] = St[i][q];
             bs_transpose(R[i]);
+            if constexpr (TW::SUB) bs_psi<TW>(R[i]);
         }
         // The staged rows are consumed before the next chunk's loads are
         // issued: the memory clobber keeps IR passes from sinking the
@@ -347,6 +380,7 @@ struct BsEncoder {
                 for (int i = 0; i < 4; i++) {
                     const int row = 4 * w + i;
                     if (row >= a.p) continue;
+                    if constexpr (TW::SUB) bs_psi<TW>(R[i]);
                     bs_transpose(R[i]);
 #ifdef RS_BS_ABL_COALESCED
                     g_u4 *q = (g_u4 *)(base - (uint64_t)lane * 64 + (uint64_t)row * a.row_stride + lane * 16);

@@ -64,7 +64,15 @@ def load_tables():
         nch = int(re.search(r"NCH = (\d+)", body).group(1))
         v = np.array([int(x, 16) for x in re.findall(r"0x([0-9a-fA-F]{4})", body)], np.uint32)
         assert v.size == (nch + 1) * 31 * 16, (k, p)
-        out[(k, p)] = (v[:nch * 496].reshape(nch, 31, 16), v[nch * 496:].reshape(31, 16))
+        sub = None
+        if "SUB = true" in body:
+            def nums(name):
+                blk = re.search(r"\b" + name + r"\[[^=]*= *(\{.*?\});", body, re.S).group(1)
+                return np.array([int(x) for x in re.findall(r"\d+", blk)], np.uint32)
+            i8, f8 = nums("ifft8"), nums("fft8")
+            assert i8.size == nch * 31 * 8 and f8.size == 31 * 8
+            sub = (nums("dmat"), i8.reshape(nch, 31, 8), f8.reshape(31, 8))
+        out[(k, p)] = (v[:nch * 496].reshape(nch, 31, 16), v[nch * 496:].reshape(31, 16), sub)
     assert out, "no geometry in bs_tables.h"
     return out
 
@@ -85,7 +93,7 @@ def gf2_apply(rows, y):
 
 def bs_encode(tabs, k, p, sym):
     """The kernel's schedule on symbols (rows of uint32 symbol values)."""
-    ifft, fft = tabs
+    ifft, fft = tabs[0], tabs[1]
 
     def i2(X, a, b, M):
         X[b] ^= X[a]
@@ -141,3 +149,37 @@ def test_tables_and_schedule_match_oracle(S):
         par = bs_encode(tabs, k, p, sym).reshape(p, -1, 32)
         got = np.concatenate([(par & 0xFF).astype(np.uint8), (par >> 8).astype(np.uint8)], axis=2).reshape(p, S)
         assert np.array_equal(got, orc.encode(16, k, p, data)), (k, p)
+
+
+def to_sub(dmat, sym):
+    """Planes r < 8 ^= XOR of planes 8+i over the bits i of dmat[r] (an involution)."""
+    out = sym.copy()
+    hi = sym >> np.uint32(8)
+    for r in range(8):
+        out ^= (np.bitwise_count(hi & np.uint32(dmat[r])) & 1).astype(np.uint32) << np.uint32(r)
+    return out
+
+
+def test_subfield_tables_match_oracle():
+    """SUB geometries: the same schedule with one 8x8 matrix on each byte half, in
+    subfield coordinates, reproduces the oracle."""
+    n = 0
+    for (k, p), (_, _, sub) in load_tables().items():
+        if sub is None:
+            continue
+        n += 1
+        dmat, i8, f8 = sub
+        # 8x8 rows -> the block-diagonal 16x16 rows the full-matrix emulation takes
+        def widen(t):
+            return (t | (t << np.uint32(8)))[..., list(range(8)) * 2] & np.concatenate(
+                [np.full(8, 0xFF, np.uint32), np.full(8, 0xFF00, np.uint32)])
+        tabs = (widen(i8), widen(f8))
+        rng = np.random.default_rng(k + p)
+        S = 128
+        data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+        blk = data.reshape(k, -1, 64)
+        sym = (blk[:, :, :32].astype(np.uint32) | (blk[:, :, 32:].astype(np.uint32) << 8)).reshape(k, -1)
+        par = to_sub(dmat, bs_encode(tabs, k, p, to_sub(dmat, sym))).reshape(p, -1, 32)
+        got = np.concatenate([(par & 0xFF).astype(np.uint8), (par >> 8).astype(np.uint8)], axis=2).reshape(p, S)
+        assert np.array_equal(got, orc.encode(16, k, p, data)), (k, p)
+    assert n >= 1
