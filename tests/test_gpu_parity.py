@@ -345,3 +345,47 @@ def test_host_pipeline_c3_pinned_matches_device(torch_dev):
     torch.cuda.synchronize()
     assert np.array_equal(dev[k:].cpu().numpy(), np.stack(shards[k:]))
     assert c.verify(shards)
+
+
+@pytest.mark.parametrize("k,p", [(128, 32), (100, 28), (10, 4)])
+def test_reconstruct_subfield_equals_full_field(torch_dev, monkeypatch, k, p):
+    """The LDS reconstruct in GF(2^8)-subfield coordinates (default for n <= 256)
+    and the full-field table path (RS_NO_SUB=1) rebuild identical bytes."""
+    torch = torch_dev
+    S = 4096 + 192
+    g = torch.Generator(device="cuda")
+    g.manual_seed(k + p)
+    full = torch.randint(0, 256, (k + p, S), dtype=torch.uint8, device="cuda", generator=g)
+    rs.New16(k, p).encode_dev(full)
+    torch.cuda.synchronize()
+    present = np.ones(k + p, bool)
+    present[np.random.default_rng(k).choice(k + p, p, replace=False)] = False
+    out = []
+    for nosub in ("0", "1"):
+        monkeypatch.setenv("RS_NO_SUB", nosub)
+        c = rs.New16(k, p)
+        broken = full.clone()
+        broken[torch.from_numpy(np.flatnonzero(~present)).cuda()] = 0
+        c.reconstruct_dev(broken, present)
+        torch.cuda.synchronize()
+        out.append(broken)
+    assert torch.equal(out[0], full) and torch.equal(out[1], full)
+
+
+def test_bitsliced_equals_split_kernel(torch_dev, monkeypatch):
+    """C3 geometry: bit-sliced kernel (default) and the split perm kernel (RS_BS=0) agree."""
+    torch = torch_dev
+    k, p, S = 128, 32, 4096 * 4
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    base = torch.randint(0, 256, (k + p, S), dtype=torch.uint8, device="cuda", generator=g)
+    outs = []
+    for bs in ("1", "0"):
+        monkeypatch.setenv("RS_BS", bs)
+        c = rs.New16(k, p)
+        assert c.encode_path == ("bs16-m32" if bs == "1" else "split16-m32")
+        slab = base.clone()
+        c.encode_dev(slab)
+        torch.cuda.synchronize()
+        outs.append(slab[k:].clone())
+    assert torch.equal(outs[0], outs[1])
