@@ -73,6 +73,16 @@ struct DeviceGuard {
         if (e_ != hipSuccess) return RS_ERR_DEVICE;  \
     } while (0)
 
+// Host half of a reconstruct (leopard16.go:432-568) for one erasure pattern:
+// which shard feeds each of the n work rows, the input scalings (errLocs),
+// which shards are rebuilt from which work row, and their output scalings.
+struct RecPlan {
+    std::vector<int> src_shard;   // n entries: shard index feeding work row r, or -1 (zero row)
+    std::vector<int> dst_shard;   // shards to rebuild, ascending
+    std::vector<int> pos;         // work row each rebuilt shard is read from
+    std::vector<uint32_t> tw_in, tw_out;
+};
+
 }  // namespace
 
 struct rs_codec {
@@ -104,10 +114,17 @@ struct rs_codec {
     DevBuf<uint8_t *> rows;         // row-pointer table (non-strided inputs)
     std::vector<uint8_t *> rows_host;
     int *hflag = nullptr, *dflag = nullptr;  // verify mismatch word: device word + pinned host readback
-    DevBuf<const uint8_t *> rc_src;
-    DevBuf<uint8_t *> rc_dst;
-    DevBuf<uint32_t> rc_tw_in, rc_tw_out;
-    DevBuf<int> rc_pos;
+    // per-call reconstruct inputs, packed into one blob and uploaded with one copy
+    DevBuf<uint8_t> rc_blob;
+    uint8_t *rc_host = nullptr;  // pinned staging of the blob
+    size_t rc_host_n = 0;
+    const uint8_t **rc_src = nullptr;
+    uint8_t **rc_dst = nullptr;
+    uint32_t *rc_tw_in = nullptr, *rc_tw_out = nullptr;
+    int *rc_pos = nullptr;
+
+    // reconstruct plans keyed by (erasure pattern, recover_all) (bounded LRU)
+    std::list<std::pair<std::vector<uint8_t>, RecPlan>> plan_cache;
 
     // error-locator cache keyed by erasure pattern (bounded LRU)
     std::list<std::pair<std::vector<uint8_t>, std::vector<uint32_t>>> el_cache;
@@ -127,7 +144,8 @@ struct rs_codec {
         work.release(); rows.release();
         if (hflag) (void)hipHostFree(hflag);
         if (dflag) (void)hipFree(dflag);
-        rc_src.release(); rc_dst.release(); rc_tw_in.release(); rc_tw_out.release(); rc_pos.release();
+        rc_blob.release();
+        if (rc_host) (void)hipHostFree(rc_host);
         if (s_in) (void)hipStreamSynchronize(s_in);
         if (s_out) (void)hipStreamSynchronize(s_out);
         stage.release();
@@ -427,17 +445,29 @@ const std::vector<uint32_t> *error_locs_cached(rs_codec *c, const std::vector<ui
     return &c->el_cache.front().second;
 }
 
-// Host half of a reconstruct (leopard16.go:432-568) for one erasure pattern:
-// which shard feeds each of the n work rows, the input scalings (errLocs),
-// which shards are rebuilt from which work row, and their output scalings.
-struct RecPlan {
-    std::vector<int> src_shard;   // n entries: shard index feeding work row r, or -1 (zero row)
-    std::vector<int> dst_shard;   // shards to rebuild, ascending
-    std::vector<int> pos;         // work row each rebuilt shard is read from
-    std::vector<uint32_t> tw_in, tw_out;
-};
 
+int plan_reconstruct_new(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, RecPlan &pl);
+
+// Plans are cached per (erasure pattern, recover_all): repeated repairs of
+// the same pattern skip the table construction.
 int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, RecPlan &pl) {
+    std::vector<uint8_t> key(present);
+    key.push_back(recover_all ? 1 : 0);
+    for (auto it = c->plan_cache.begin(); it != c->plan_cache.end(); ++it) {
+        if (it->first == key) {
+            c->plan_cache.splice(c->plan_cache.begin(), c->plan_cache, it);
+            pl = c->plan_cache.front().second;
+            return RS_OK;
+        }
+    }
+    int e = plan_reconstruct_new(c, present, recover_all, pl);
+    if (e) return e;
+    c->plan_cache.emplace_front(std::move(key), pl);
+    if (c->plan_cache.size() > 16) c->plan_cache.pop_back();
+    return RS_OK;
+}
+
+int plan_reconstruct_new(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, RecPlan &pl) {
     int e = build_decode_plan(c);
     if (e) return e;
     if (!c->dec_ok) return RS_ERR_PANIC;
@@ -482,29 +512,42 @@ int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool reco
     return RS_OK;
 }
 
-// Upload a plan for `nsets` row-pointer sets (set b: shard i at d[b][i]).
-// The host vectors must stay alive until the stream has consumed them.
-int upload_reconstruct(rs_codec *c, const RecPlan &pl, const std::vector<uint8_t *const *> &d,
-                       std::vector<const uint8_t *> &src_h, std::vector<uint8_t *> &dst_h, hipStream_t s) {
-    const int n = c->n, nd = (int)pl.dst_shard.size(), ns = (int)d.size();
-    src_h.assign((size_t)ns * n, nullptr);
-    dst_h.assign((size_t)ns * std::max(nd, 1), nullptr);
-    for (int b = 0; b < ns; b++) {
-        for (int r = 0; r < n; r++)
-            if (pl.src_shard[r] >= 0) src_h[(size_t)b * n + r] = d[b][pl.src_shard[r]];
-        for (int j = 0; j < nd; j++) dst_h[(size_t)b * std::max(nd, 1) + j] = d[b][pl.dst_shard[j]];
+// Upload a plan for `nsets` row-pointer sets (set b: shard i at d[b][i]) as
+// one packed blob: row pointers, scale tables, rebuilt-row positions.  The
+// pinned staging buffer is reused by the next call; every caller synchronizes
+// its stream before returning (calls are serialized by the codec mutex).
+int upload_reconstruct(rs_codec *c, const RecPlan &pl, const std::vector<uint8_t *const *> &d, hipStream_t s) {
+    const int n = c->n, nd = (int)pl.dst_shard.size(), ns = (int)d.size(), ndd = std::max(nd, 1);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t s_src = (size_t)ns * n * sizeof(void *), s_dst = (size_t)ns * ndd * sizeof(void *);
+    const size_t s_in = pl.tw_in.size() * 4, s_out = pl.tw_out.size() * 4, s_pos = std::max<size_t>(pl.pos.size(), 1) * 4;
+    const size_t o_dst = al(s_src), o_in = o_dst + al(s_dst), o_out = o_in + al(s_in), o_pos = o_out + al(s_out);
+    const size_t total = o_pos + al(s_pos);
+    HIP_TRY(c->rc_blob.ensure(total));
+    if (c->rc_host_n < total) {
+        if (c->rc_host) HIP_TRY(hipHostFree(c->rc_host));
+        c->rc_host = nullptr;
+        c->rc_host_n = 0;
+        HIP_TRY(hipHostMalloc((void **)&c->rc_host, total, hipHostMallocDefault));
+        c->rc_host_n = total;
     }
-    HIP_TRY(c->rc_src.ensure(src_h.size()));
-    HIP_TRY(c->rc_dst.ensure(dst_h.size()));
-    HIP_TRY(c->rc_tw_in.ensure(pl.tw_in.size()));
-    HIP_TRY(c->rc_tw_out.ensure(pl.tw_out.size()));
-    HIP_TRY(c->rc_pos.ensure(std::max<size_t>(pl.pos.size(), 1)));
-    HIP_TRY(hipMemcpyAsync(c->rc_src.p, src_h.data(), src_h.size() * sizeof(void *), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(c->rc_dst.p, dst_h.data(), dst_h.size() * sizeof(void *), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(c->rc_tw_in.p, pl.tw_in.data(), pl.tw_in.size() * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(c->rc_tw_out.p, pl.tw_out.data(), pl.tw_out.size() * 4, hipMemcpyHostToDevice, s));
-    if (!pl.pos.empty())
-        HIP_TRY(hipMemcpyAsync(c->rc_pos.p, pl.pos.data(), pl.pos.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    uint8_t *h = c->rc_host;
+    const uint8_t **src = (const uint8_t **)h;
+    uint8_t **dst = (uint8_t **)(h + o_dst);
+    for (int b = 0; b < ns; b++) {
+        for (int r = 0; r < n; r++) src[(size_t)b * n + r] = pl.src_shard[r] >= 0 ? d[b][pl.src_shard[r]] : nullptr;
+        for (int j = 0; j < ndd; j++) dst[(size_t)b * ndd + j] = j < nd ? d[b][pl.dst_shard[j]] : nullptr;
+    }
+    std::memcpy(h + o_in, pl.tw_in.data(), s_in);
+    std::memcpy(h + o_out, pl.tw_out.data(), s_out);
+    if (!pl.pos.empty()) std::memcpy(h + o_pos, pl.pos.data(), pl.pos.size() * 4);
+    HIP_TRY(hipMemcpyAsync(c->rc_blob.p, h, total, hipMemcpyHostToDevice, s));
+    uint8_t *g = c->rc_blob.p;
+    c->rc_src = (const uint8_t **)g;
+    c->rc_dst = (uint8_t **)(g + o_dst);
+    c->rc_tw_in = (uint32_t *)(g + o_in);
+    c->rc_tw_out = (uint32_t *)(g + o_out);
+    c->rc_pos = (int *)(g + o_pos);
     return RS_OK;
 }
 
@@ -514,11 +557,11 @@ int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipS
     if (c->logn <= kMaxLdsLogN) {  // whole transform LDS-resident: one HBM read/write per row
         if (!nd) return RS_OK;
         RecArgs ra{};
-        ra.src = c->rc_src.p + (size_t)set * n;
-        ra.dst = c->rc_dst.p + (size_t)set * nd;
-        ra.pos = c->rc_pos.p;
-        ra.tw_in = c->rc_tw_in.p;
-        ra.tw_out = c->rc_tw_out.p;
+        ra.src = c->rc_src + (size_t)set * n;
+        ra.dst = c->rc_dst + (size_t)set * nd;
+        ra.pos = c->rc_pos;
+        ra.tw_in = c->rc_tw_in;
+        ra.tw_out = c->rc_tw_out;
         ra.tw_ifft = c->dtw_ifft.p;
         ra.tw_fft = c->dtw_fft.p;
         ra.S = S;
@@ -529,13 +572,13 @@ int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipS
     }
     HIP_TRY(c->work.ensure((size_t)n * S));
     uint8_t *w = c->work.p;
-    HIP_TRY(launch_scale_in(c->bits, w, S, c->rc_src.p + (size_t)set * n, c->rc_tw_in.p, n, s));
+    HIP_TRY(launch_scale_in(c->bits, w, S, c->rc_src + (size_t)set * n, c->rc_tw_in, n, s));
     int e = run_passes(c, true, w, S, c->logn, c->m + c->k, c->dtw_ifft.p, s);
     if (e) return e;
     HIP_TRY(launch_formal_derivative(c->bits, w, S, n, s));
     e = run_passes(c, false, w, S, c->logn, c->m + c->k, c->dtw_fft.p, s);
     if (e) return e;
-    if (nd) HIP_TRY(launch_reveal(c->bits, c->rc_dst.p + (size_t)set * nd, w, S, c->rc_pos.p, c->rc_tw_out.p, nd, s));
+    if (nd) HIP_TRY(launch_reveal(c->bits, c->rc_dst + (size_t)set * nd, w, S, c->rc_pos, c->rc_tw_out, nd, s));
     return RS_OK;
 }
 
@@ -545,13 +588,11 @@ int reconstruct_device(rs_codec *c, uint8_t *const *d, const std::vector<uint8_t
     RecPlan pl;
     int e = plan_reconstruct(c, present, recover_all, pl);
     if (e) return e;
-    std::vector<const uint8_t *> src_h;
-    std::vector<uint8_t *> dst_h;
-    e = upload_reconstruct(c, pl, {d}, src_h, dst_h, s);
+    e = upload_reconstruct(c, pl, {d}, s);
     if (e) return e;
     e = launch_reconstruct(c, pl, 0, S, s);
     if (e) return e;
-    HIP_TRY(hipStreamSynchronize(s));  // host vectors above must outlive the async copies
+    HIP_TRY(hipStreamSynchronize(s));  // the pinned staging of the upload is reused by the next call
     return RS_OK;
 }
 
@@ -654,8 +695,6 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     // scratch of the multi-pass paths, sized before any launch (no realloc mid-pipeline)
     if (op == HostOp::Reconstruct) HIP_TRY(c->work.ensure((size_t)c->n * seg));
     else if (c->logm > kMaxRegLogM) HIP_TRY(c->work.ensure((size_t)2 * c->m * seg));
-    std::vector<const uint8_t *> src_h;
-    std::vector<uint8_t *> dst_h;
     std::vector<std::vector<uint8_t *>> sets(kHostBufs, std::vector<uint8_t *>(total));
     if (op == HostOp::Reconstruct) {
         std::vector<uint8_t *const *> d;
@@ -663,7 +702,7 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
             for (int i = 0; i < total; i++) sets[b][i] = c->stage.p + b * slab + (uint64_t)i * seg;
             d.push_back(sets[b].data());
         }
-        e = upload_reconstruct(c, pl, d, src_h, dst_h, sc);
+        e = upload_reconstruct(c, pl, d, sc);
         if (e) return e;
     }
     if (op == HostOp::Verify) HIP_TRY(hipMemsetAsync(c->dflag, 0, sizeof(int), sc));
