@@ -1160,8 +1160,12 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 // 16 low bytes + the 16 high bytes 32 bytes later) or F8<4> (16 bytes).
 // Twiddle tables come from global memory (identical for every workgroup, so
 // they stay in L1/L2).
-constexpr int kTileB = 128;   // bytes of each row owned by a workgroup
-constexpr int kLdsRow = 144;  // LDS row stride: 36 dwords spreads rows over the banks
+#ifndef RS_LDS_TILE
+#define RS_LDS_TILE 128
+#endif
+constexpr int kTileB = RS_LDS_TILE;        // bytes of each row owned by a workgroup
+constexpr int kLdsRow = RS_LDS_TILE + 16;  // LDS row stride (144 B = 36 dwords spreads rows over the banks)
+constexpr int kLdsW = RS_LDS_TILE / 32;    // unit width: F16<kLdsW> units of 8*kLdsW bytes, 4 units per tile
 
 template <class F>
 struct LTile {
@@ -1568,12 +1572,12 @@ hipError_t launch_reveal(int bits, uint8_t *const *dst, const uint8_t *work, uin
 
 
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s) {
-    if (bits != 16) return rec_lds_f<F8<4>>(logn, a, s);
-    return sub ? rec_lds_f<F16<4>, F16S<4>>(logn, a, s) : rec_lds_f<F16<4>>(logn, a, s);
+    if (bits != 16) return rec_lds_f<F8<kLdsW>>(logn, a, s);
+    return sub ? rec_lds_f<F16<kLdsW>, F16S<kLdsW>>(logn, a, s) : rec_lds_f<F16<kLdsW>>(logn, a, s);
 }
 
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
-    return bits == 16 ? enc_lds_f<F16<4>>(logm, verify, a, s) : enc_lds_f<F8<4>>(logm, verify, a, s);
+    return bits == 16 ? enc_lds_f<F16<kLdsW>>(logm, verify, a, s) : enc_lds_f<F8<kLdsW>>(logm, verify, a, s);
 }
 
 }  // namespace rs
