@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes as C
 import io
+import sys
 from typing import Optional, Sequence
 
 import numpy as np
@@ -76,6 +77,7 @@ class _PinnedBlock:
     """Owner of one rs_host_alloc block; freed when the last view dies."""
 
     def __init__(self, nbytes: int):
+        self.ptr = None
         L = _capi.lib()
         p = C.c_void_p()
         _check(L.rs_host_alloc(nbytes, C.byref(p)))
@@ -158,13 +160,12 @@ class ReedSolomon:
         L = _capi.lib()
         if device is None:
             device = 0
-            try:
-                import torch
-
-                if torch.cuda.is_available():
-                    device = torch.cuda.current_device()
-            except Exception:
-                pass
+            # follow torch's current device only when the caller already uses
+            # torch: importing it here, after this library has loaded the HIP
+            # runtime, made the first pinned allocation of a torch-free process fail
+            torch = sys.modules.get("torch")
+            if torch is not None and torch.cuda.is_available():
+                device = torch.cuda.current_device()
         h = C.c_void_p()
         _check(L.rs_new(field_bits, data_shards, parity_shards, device, C.byref(h)))
         self._h = h
@@ -241,7 +242,7 @@ class ReedSolomon:
         bufs = list(shards)
         for i in range(min(end, total)):
             if bufs[i] is None or len(bufs[i]) == 0:
-                bufs[i] = np.zeros(S, dtype=np.uint8)  # Go: make([]byte, shardSize)
+                bufs[i] = np.empty(S, dtype=np.uint8)  # Go: make([]byte, shardSize); fully overwritten
         ptrs = (C.c_void_p * total)()
         lens = (C.c_size_t * total)()
         for i, s in enumerate(shards):

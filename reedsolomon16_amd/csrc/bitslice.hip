@@ -256,6 +256,8 @@ struct BsEncoder {
                 for (int q = 0; q < 4; q++) {
 #ifdef RS_BS_ABL_COALESCED  // same bytes, lane-contiguous 16-byte pieces (wrong layout)
                     const u32x4 x = *(gc_u4 *)(base - (uint64_t)lane * 64 + (uint64_t)row * a.row_stride + q * 1024 + lane * 16);
+#elif defined(RS_BS_NT_LOAD)  // streamed once: non-temporal policy
+                    const u32x4 x = __builtin_nontemporal_load(p + q);
 #else
                     const u32x4 x = p[q];
 #endif
@@ -399,7 +401,11 @@ struct BsEncoder {
                             const u32x4 o = q[kq];
                             bad |= (o[0] ^ v[0]) | (o[1] ^ v[1]) | (o[2] ^ v[2]) | (o[3] ^ v[3]);
                         } else {
+#ifdef RS_BS_NT_STORE
+                            __builtin_nontemporal_store(v, q + kq);
+#else
                             q[kq] = v;
+#endif
                         }
                     }
                 }

@@ -31,7 +31,7 @@ namespace {
 constexpr int kMaxRegLogM = 5;  // m <= 32: fused register kernel
 constexpr int kMaxLdsLogN = 8;  // n (or m) <= 256: LDS-resident transform kernels
 constexpr int kHostBufs = 3;    // staging slabs of the host-resident pipeline
-constexpr uint64_t kHostSegTarget = 8ull << 20;  // bytes copied in per segment
+constexpr uint64_t kHostSegTarget = 32ull << 20;  // bytes copied in per segment (scripts/host_seg_sweep.py: 256 KiB rows at 128+32)
 
 template <class T>
 struct DevBuf {
@@ -135,6 +135,9 @@ struct rs_codec {
     hipEvent_t ev_in[kHostBufs] = {}, ev_k[kHostBufs] = {}, ev_free[kHostBufs] = {};
     DevBuf<uint8_t> stage;
     uint64_t host_seg_bytes = 0;  // 0: automatic
+    // pinned bounce slabs for outputs in pageable host memory (kHostBufs x total x seg)
+    uint8_t *bounce = nullptr;
+    size_t bounce_n = 0;
 
     ~rs_codec() {
         if (!dev_ready && !stream) return;
@@ -149,6 +152,7 @@ struct rs_codec {
         if (s_in) (void)hipStreamSynchronize(s_in);
         if (s_out) (void)hipStreamSynchronize(s_out);
         stage.release();
+        if (bounce) (void)hipHostFree(bounce);
         for (int b = 0; b < kHostBufs; b++) {
             if (ev_in[b]) (void)hipEventDestroy(ev_in[b]);
             if (ev_k[b]) (void)hipEventDestroy(ev_k[b]);
@@ -670,6 +674,20 @@ int copy_rows(uint8_t *dev, uint64_t dpitch, uint8_t *const *host, const std::ve
 
 enum class HostOp { Encode, Verify, Reconstruct };
 
+// True when `p` is ordinary pageable host memory (not hipHostMalloc'd or
+// registered).  Device-to-host copies into such memory are staged by the
+// driver one small copy at a time, which is what made the reconstruct of
+// freshly allocated output shards (Go's make([]byte, S), leopard16.go:556-560)
+// run at a few GB/s.
+bool is_pageable(const void *p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;
+    }
+    return at.type != hipMemoryTypeHost && at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeManaged;
+}
+
 int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, const std::vector<uint8_t> &present,
                   bool recover_all, int *ok) {
     int e = ensure_host_pipe(c);
@@ -695,6 +713,30 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     // scratch of the multi-pass paths, sized before any launch (no realloc mid-pipeline)
     if (op == HostOp::Reconstruct) HIP_TRY(c->work.ensure((size_t)c->n * seg));
     else if (c->logm > kMaxRegLogM) HIP_TRY(c->work.ensure((size_t)2 * c->m * seg));
+    // outputs in pageable memory go D2H into a pinned bounce slab, and the host
+    // copies segment j - 1 out while the device works on segment j
+    bool use_bounce = false;
+    for (int r : out_rows) use_bounce = use_bounce || is_pageable(shards[r]);
+    std::vector<std::vector<uint8_t *>> btab(kHostBufs, std::vector<uint8_t *>(total));
+    if (use_bounce) {
+        const size_t need = (size_t)kHostBufs * slab;
+        if (c->bounce_n < need) {
+            if (c->bounce) HIP_TRY(hipHostFree(c->bounce));
+            c->bounce = nullptr;
+            c->bounce_n = 0;
+            HIP_TRY(hipHostMalloc((void **)&c->bounce, need, hipHostMallocDefault));
+            c->bounce_n = need;
+        }
+        for (int b = 0; b < kHostBufs; b++)
+            for (int i = 0; i < total; i++) btab[b][i] = c->bounce + b * slab + (uint64_t)i * seg;
+    }
+    auto drain = [&](uint64_t j) -> int {  // host copy of segment j's outputs out of its bounce slab
+        const int b = (int)(j % kHostBufs);
+        const uint64_t off = j * seg, w = std::min(seg, S - off);
+        HIP_TRY(hipEventSynchronize(c->ev_free[b]));
+        for (int r : out_rows) std::memcpy(shards[r] + off, btab[b][r], w);
+        return RS_OK;
+    };
     std::vector<std::vector<uint8_t *>> sets(kHostBufs, std::vector<uint8_t *>(total));
     if (op == HostOp::Reconstruct) {
         std::vector<uint8_t *const *> d;
@@ -729,14 +771,23 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
         HIP_TRY(hipEventRecord(c->ev_k[b], sc));
         if (!out_rows.empty()) {
             HIP_TRY(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0));
-            e = copy_rows(st, seg, shards, out_rows, off, w, false, c->s_out);
+            if (use_bounce) e = copy_rows(st, seg, btab[b].data(), out_rows, 0, w, false, c->s_out);
+            else e = copy_rows(st, seg, shards, out_rows, off, w, false, c->s_out);
             if (e) return e;
             HIP_TRY(hipEventRecord(c->ev_free[b], c->s_out));
+            if (use_bounce && j > 0) {
+                e = drain(j - 1);
+                if (e) return e;
+            }
         } else {
             HIP_TRY(hipEventRecord(c->ev_free[b], sc));
         }
     }
     if (op == HostOp::Verify) HIP_TRY(hipMemcpyAsync(c->hflag, c->dflag, sizeof(int), hipMemcpyDeviceToHost, sc));
+    if (use_bounce && nseg) {
+        e = drain(nseg - 1);
+        if (e) return e;
+    }
     HIP_TRY(hipStreamSynchronize(c->s_in));
     HIP_TRY(hipStreamSynchronize(sc));
     HIP_TRY(hipStreamSynchronize(c->s_out));
