@@ -1,6 +1,6 @@
 #!/bin/bash
 # Bit-sliced kernel ablations (performance experiments only): one library per
-# variant in build/ablate_bs/<name>/, 128+32 geometry only.
+# variant in build/ablate_bs/<name>/, every compiled-in geometry (BS_CONFIGS).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 set -e
 HIPCC=/opt/rocm/bin/hipcc
@@ -8,7 +8,7 @@ SRC=reedsolomon16_amd/csrc
 B=reedsolomon16_amd/build
 OUT=build/ablate_bs
 rm -rf $OUT; mkdir -p $OUT/common
-$B/gen_bs_tables $OUT/common/bs_tables.h 128:32
+$B/gen_bs_tables $OUT/common/bs_tables.h ${BS_CONFIGS:-128:32 32:32 100:17}
 for v in ${VARIANTS:-base: nomul:-DRS_BS_ABL_NOMUL nolds:-DRS_BS_ABL_NOLDS noload:-DRS_BS_ABL_NOLOAD notrans:-DRS_BS_ABL_NOTRANS}; do
   name=${v%%:*}; flags=${v#*:}; flags=${flags//,/ }
   mkdir -p $OUT/$name
