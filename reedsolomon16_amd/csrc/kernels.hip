@@ -1457,12 +1457,19 @@ hipError_t launch_encode_reg(int bits, int logm, bool verify, const EncodeArgs &
             case 5: return enc_reg<F16<1>, 5>(verify, a, s);
         }
     } else {
+        // Small GF(2^8) stripes (C2: 10+4 x 1 MiB is 256 workgroups of 16-byte
+        // units, one per CU, latency-bound): 4-byte units give 4x the
+        // workgroups and 4x the loads in flight per CU.
+#ifndef RS_F8_NARROW
+#define RS_F8_NARROW 1
+#endif
+        const bool narrow = RS_F8_NARROW && (a.shard_size / 16 + 255) / 256 * (uint64_t)a.nstripes < 1024;
         switch (logm) {
             case 0: return enc_reg<F8<4>, 0>(verify, a, s);
             case 1: return enc_reg<F8<4>, 1>(verify, a, s);
-            case 2: return enc_reg<F8<4>, 2>(verify, a, s);
-            case 3: return enc_reg<F8<4>, 3>(verify, a, s);
-            case 4: return enc_reg<F8<4>, 4>(verify, a, s);
+            case 2: return narrow ? enc_reg<F8<1>, 2>(verify, a, s) : enc_reg<F8<4>, 2>(verify, a, s);
+            case 3: return narrow ? enc_reg<F8<1>, 3>(verify, a, s) : enc_reg<F8<4>, 3>(verify, a, s);
+            case 4: return narrow ? enc_reg<F8<1>, 4>(verify, a, s) : enc_reg<F8<4>, 4>(verify, a, s);
             case 5: return enc_reg<F8<2>, 5>(verify, a, s);
         }
     }

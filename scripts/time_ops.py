@@ -14,6 +14,10 @@ CONFIGS = {
     "C4": (16, 128, 32, 1 << 20, "reconstruct"),
     "C5": (16, 1024, 256, 256 << 10, "encode"),
     "C5x8": (16, 1024, 256, 32 << 10, "encode"),
+    # encode batches: stripes per launch (rs_encode_dev_batch), so a small
+    # stripe's kernel time is not hidden behind the per-call host cost
+    "C2x16": (8, 10, 4, 1 << 20, "encode", 16),
+    "C3x16": (16, 128, 32, 1 << 20, "encode", 16),
 }
 # Host-resident (PCIe-inclusive) variants: shards in host memory, rs_encode /
 # rs_reconstruct stream them through the GPU.  "p" = pinned rows (rs_host_alloc).
@@ -76,9 +80,10 @@ def main():
         if name in HOST_CONFIGS:
             time_host(name, max(5, a.iters // 5), a.tag)
             continue
-        bits, k, p, S, op = CONFIGS[name]
+        bits, k, p, S, op = CONFIGS[name][:5]
+        ns = CONFIGS[name][5] if len(CONFIGS[name]) > 5 else 1
         c = rs.ReedSolomon(k, p, bits)
-        slab = torch.randint(0, 256, (1, k + p, S), dtype=torch.uint8, device="cuda")
+        slab = torch.randint(0, 256, (ns, k + p, S), dtype=torch.uint8, device="cuda")
         rows = slab[0]
         present = np.ones(k + p, bool)
         present[np.random.default_rng(0x5EED).choice(k + p, p, replace=False)] = False
@@ -101,7 +106,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.iters
-        alg = (k + p) * S
+        alg = ns * (k + p) * S
         print(json.dumps({"tag": a.tag, "config": name, "op": op, "path": c.encode_path, "us": round(us, 2),
                           "GBps_alg": round(alg / us / 1e3, 1), "frac": round(alg / us / 1e3 / 8000, 4)}), flush=True)
 
