@@ -389,3 +389,33 @@ def test_bitsliced_equals_split_kernel(torch_dev, monkeypatch):
         torch.cuda.synchronize()
         outs.append(slab[k:].clone())
     assert torch.equal(outs[0], outs[1])
+
+
+# Host reconstruct whose output rows are pinned (a C caller's preallocated
+# rows): the rebuilt rows go device -> host directly; fresh pageable rows (the
+# Python mirror, Go's make) go through the pinned bounce slab.  Both at C4's
+# size with the default segment width (several segments).
+@pytest.mark.parametrize("outputs", ["pinned", "pageable"])
+def test_host_reconstruct_c4_output_memory(outputs):
+    import ctypes as C
+
+    from reedsolomon16_amd import codec as rc
+
+    k, p, S = 128, 32, 1 << 20
+    c = rs.New16(k, p)
+    shards = c.alloc_aligned(S, pinned=True)
+    rng = np.random.default_rng(4)
+    for i in range(k):
+        shards[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+    c.encode(shards)
+    full = [s.copy() for s in shards]
+    er = sorted(rng.choice(k + p, p, replace=False).tolist())
+    outs = {i: (rc.alloc_pinned(S) if outputs == "pinned" else np.empty(S, np.uint8)) for i in er}
+    for o in outs.values():
+        o[:] = 0xA5
+    ptrs = (C.c_void_p * (k + p))(*[(outs[i] if i in outs else shards[i]).ctypes.data for i in range(k + p)])
+    lens = (C.c_size_t * (k + p))(*[0 if i in outs else S for i in range(k + p)])
+    assert c._L.rs_reconstruct(c._h, ptrs, lens, k + p, 1) == 0
+    for i in er:
+        assert lens[i] == S
+        assert np.array_equal(outs[i], full[i]), i
