@@ -40,6 +40,15 @@
 #include "kernels.hpp"
 
 namespace rs {
+// RS_BS_STAMP (diagnostic builds only, scripts/bs_stamps.py): per wave,
+// s_memtime totals of the load wait at each chunk start, the LDS barriers,
+// the final FFT + stores, and the whole run, written once per launch.
+#ifndef RS_BS_STAMP
+#define RS_BS_STAMP 0
+#endif
+#if RS_BS_STAMP
+__device__ unsigned long long g_bs_stamps[1024 * 8 * 4];
+#endif
 namespace {
 
 typedef uint32_t Planes[16];
@@ -235,6 +244,18 @@ struct BsEncoder {
     Planes St[4];    // staged data rows (64-byte blocks as loaded)
     Planes R[4];     // working rows (bit-planes)
     Planes A[3];     // accumulator rows w, w + 8, w + 16 (row w + 24's: LDS row 32 + w)
+#if RS_BS_STAMP
+    unsigned long long t_load = 0, t_bar = 0, t_fft = 0, t_total = 0;
+#endif
+    __device__ __forceinline__ void bar() {
+#if RS_BS_STAMP
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        lds_barrier();
+        t_bar += __builtin_amdgcn_s_memtime() - t0;
+#else
+        lds_barrier();
+#endif
+    }
 
     // Load rows 32c + 4w + i of `tile` (zero past k, past the row end, past the last tile).
     __device__ __forceinline__ void stage(int tile, int c) {
@@ -276,6 +297,13 @@ struct BsEncoder {
     template <int C>
     __device__ __forceinline__ void chunk(int tile) {
         __builtin_amdgcn_sched_barrier(0);
+#if RS_BS_STAMP  // the compiler waits vmcnt(0) here anyway (chunk 0 included)
+        {
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            t_load += __builtin_amdgcn_s_memtime() - t0;
+        }
+#endif
 #pragma unroll
         for (int i = 0; i < 4; i++) {
 #pragma unroll
@@ -297,10 +325,10 @@ struct BsEncoder {
         __builtin_amdgcn_sched_barrier(0);
         // pass 1: rows 4w + i, radix-4 at dist 1 (group w, slots 3w..3w+2)
         dispatch<8>(w, [&](auto W) { bs_ifft4<TW, C, 3 * decltype(W)::value>(R); });
-        lds_barrier();  // previous readers of the image are done
+        bar();  // previous readers of the image are done
 #pragma unroll
         for (int i = 0; i < 4; i++) lds_put(lbase, 4 * w + i, R[i]);
-        lds_barrier();
+        bar();
         // pass 2: rows 16h + j + 4i, radix-4 at dist 4 (group h, slots 24 + 3h ..)
         const int h = w >> 2, j = w & 3;
 #pragma unroll
@@ -308,7 +336,7 @@ struct BsEncoder {
         dispatch<2>(h, [&](auto H) { bs_ifft4<TW, C, 24 + 3 * decltype(H)::value>(R); });
 #pragma unroll
         for (int i = 0; i < 4; i++) lds_put(lbase, 16 * h + j + 4 * i, R[i]);
-        lds_barrier();
+        bar();
         // pass 3: rows w + 8i, radix-2 at dist 16 (slot 30): pairs (w, w+16), (w+8, w+24)
 #pragma unroll
         for (int i = 0; i < 4; i++) lds_get(lbase, w + 8 * i, R[i]);
@@ -340,10 +368,16 @@ struct BsEncoder {
     }
 
     __device__ __forceinline__ void run() {
+#if RS_BS_STAMP
+        const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
         int tile = blockIdx.x;
         stage(tile, 0);
         for (; tile < a.ntiles; tile += gridDim.x) {
             chunks(tile, std::make_integer_sequence<int, NCH>{});
+#if RS_BS_STAMP
+            const unsigned long long t_f0 = __builtin_amdgcn_s_memtime();
+#endif
             // FFT pass A: rows w + 8i (dist 16 then 8; the only group: slots 0..2)
 #pragma unroll
             for (int i = 0; i < 3; i++)
@@ -351,10 +385,10 @@ struct BsEncoder {
                 for (int q = 0; q < 16; q++) R[i][q] = A[i][q];
             lds_get(lbase, 32 + w, R[3]);
             bs_fft4<TW, 0>(R);
-            lds_barrier();
+            bar();
 #pragma unroll
             for (int i = 0; i < 4; i++) lds_put(lbase, w + 8 * i, R[i]);
-            lds_barrier();
+            bar();
             // pass B: rows 8g + j + 2i (dist 4 then 2; group g, slots 3 + 3g ..)
             const int g = w >> 1, j = w & 1;
 #pragma unroll
@@ -362,7 +396,7 @@ struct BsEncoder {
             dispatch<4>(g, [&](auto G) { bs_fft4<TW, 3 + 3 * decltype(G)::value>(R); });
 #pragma unroll
             for (int i = 0; i < 4; i++) lds_put(lbase, 8 * g + j + 2 * i, R[i]);
-            lds_barrier();
+            bar();
             // pass C: rows 4w + i, radix-2 at dist 1 (slots 15 + 2w, 16 + 2w)
 #pragma unroll
             for (int i = 0; i < 4; i++) lds_get(lbase, 4 * w + i, R[i]);
@@ -410,6 +444,9 @@ struct BsEncoder {
                     }
                 }
             }
+#if RS_BS_STAMP
+            t_fft += __builtin_amdgcn_s_memtime() - t_f0;
+#endif
             if constexpr (VERIFY) {
                 // one store per wave, not per lane
                 const uint64_t m = __ballot(bad != 0);
@@ -417,6 +454,9 @@ struct BsEncoder {
                     __hip_atomic_store(a.mismatch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+#if RS_BS_STAMP
+        t_total = __builtin_amdgcn_s_memtime() - t_start;
+#endif
     }
 };
 
@@ -429,6 +469,15 @@ __global__ void __launch_bounds__(512, 2) k_encode_bs(BsArgs a) {
     e.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     e.lbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)lds + e.lane * 16;
     e.run();
+#if RS_BS_STAMP
+    if (e.lane == 0 && blockIdx.x < 1024) {
+        unsigned long long *o = g_bs_stamps + (blockIdx.x * 8 + e.w) * 4;
+        o[0] = e.t_load;
+        o[1] = e.t_bar;
+        o[2] = e.t_fft;
+        o[3] = e.t_total;
+    }
+#endif
 }
 
 template <class TW>
@@ -455,5 +504,11 @@ hipError_t launch_encode_bs(bool verify, const BsArgs &a, int grid, hipStream_t 
 #undef RS_BS_LAUNCH
     return hipErrorNotSupported;
 }
+
+#if RS_BS_STAMP
+extern "C" int rs_debug_bs_stamps(unsigned long long *out, size_t n) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bs_stamps), n * sizeof(unsigned long long));
+}
+#endif
 
 }  // namespace rs
