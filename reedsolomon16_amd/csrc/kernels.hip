@@ -1160,22 +1160,24 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 // 16 low bytes + the 16 high bytes 32 bytes later) or F8<4> (16 bytes).
 // Twiddle tables come from global memory (identical for every workgroup, so
 // they stay in L1/L2).
-#ifndef RS_LDS_TILE
-#define RS_LDS_TILE 128
-#endif
-constexpr int kTileB = RS_LDS_TILE;        // bytes of each row owned by a workgroup
-constexpr int kLdsRow = RS_LDS_TILE + 16;  // LDS row stride (144 B = 36 dwords spreads rows over the banks)
-constexpr int kLdsW = RS_LDS_TILE / 32;    // unit width: F16<kLdsW> units of 8*kLdsW bytes, 4 units per tile
+// Tile width per unit type: 4 units of F16<W> (8W bytes) or 8 of F8<W> (4W
+// bytes), i.e. 32W bytes of each row per workgroup.  The launchers use
+// 128-byte tiles (W = 4), or 64-byte tiles (W = 2) when 128-byte tiles would
+// give fewer than kLdsMinGrid workgroups (C5's 32 KiB per-GPU byte range:
+// 57.0 -> 52.8 us; full-size C4 / C5 are faster at 128 bytes).
+constexpr uint64_t kLdsMinGrid = 512;
 
 template <class F>
 struct LTile {
     static constexpr bool W16 = F::SYM16;
+    static constexpr int TB = 32 * F::W;                  // bytes of each row owned by a workgroup
+    static constexpr int ROW = TB + 16;                   // LDS row stride (144 B at TB = 128 spreads rows over the banks)
     static constexpr int UB = W16 ? 8 * F::W : 4 * F::W;  // global bytes per unit
-    static constexpr int U = kTileB / UB;                 // units per tile
+    static constexpr int U = TB / UB;                     // units per tile
     typedef typename F::Vec V;
     __device__ static V get(const uint8_t *lds, int row, int u) {
         V v;
-        const uint8_t *p = lds + row * kLdsRow + F::off(u);
+        const uint8_t *p = lds + row * ROW + F::off(u);
         if constexpr (W16) {
             ldw_lds<F::W>(p, v.l);
             ldw_lds<F::W>(p + 32, v.h);
@@ -1186,7 +1188,7 @@ struct LTile {
     }
     __device__ static void put(uint8_t *lds, int row, int u, const V &v) {
         typedef typename VecOf<F::W>::T T;
-        uint8_t *p = lds + row * kLdsRow + F::off(u);
+        uint8_t *p = lds + row * ROW + F::off(u);
         auto st = [](uint8_t *q, const uint32_t(&w)[F::W]) {
             T x;
             if constexpr (F::W == 1) x = w[0];
@@ -1290,8 +1292,8 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     typedef typename F::Vec V;
     constexpr int N = 1 << LOGN, U = L::U;
     constexpr int K = (N * U + 255) / 256;  // derivative outputs per thread
-    __shared__ __attribute__((aligned(16))) uint8_t lds[N * kLdsRow];
-    const uint64_t tile = (uint64_t)blockIdx.x * kTileB;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[N * L::ROW];
+    const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
     // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0
     for (int it = threadIdx.x; it < N * U; it += 256) {
         const int r = it / U, u = it - r * U;
@@ -1345,8 +1347,8 @@ __global__ void __launch_bounds__(256) k_enc_lds(EncodeArgs a) {
     typedef typename F::Vec V;
     constexpr int M = 1 << LOGM, U = L::U;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-    uint8_t *acc = lds_dyn, *cur = lds_dyn + M * kLdsRow;
-    const uint64_t tile = (uint64_t)blockIdx.x * kTileB;
+    uint8_t *acc = lds_dyn, *cur = lds_dyn + M * L::ROW;
+    const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
     const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
     constexpr int its = ifft_slot_count(LOGM);
     for (int c = 0; c < a.nchunks; c++) {
@@ -1387,7 +1389,7 @@ __global__ void __launch_bounds__(256) k_enc_lds(EncodeArgs a) {
 
 template <class F, class FT, int LOGN>
 hipError_t rec_lds_t(const RecArgs &a, hipStream_t s) {
-    const dim3 grid((unsigned)((a.S + kTileB - 1) / kTileB));
+    const dim3 grid((unsigned)((a.S + LTile<F>::TB - 1) / LTile<F>::TB));
     hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
@@ -1408,8 +1410,8 @@ hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
 
 template <class F, int LOGM>
 hipError_t enc_lds_t(bool verify, const EncodeArgs &a, hipStream_t s) {
-    const dim3 grid((unsigned)((a.shard_size + kTileB - 1) / kTileB), (unsigned)a.nstripes);
-    const size_t lds = (size_t)2 * (1 << LOGM) * kLdsRow;
+    const dim3 grid((unsigned)((a.shard_size + LTile<F>::TB - 1) / LTile<F>::TB), (unsigned)a.nstripes);
+    const size_t lds = (size_t)2 * (1 << LOGM) * LTile<F>::ROW;
     if (verify) {
         (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL((k_enc_lds<F, LOGM, true>), grid, dim3(256), lds, s, a);
@@ -1578,13 +1580,20 @@ hipError_t launch_reveal(int bits, uint8_t *const *dst, const uint8_t *work, uin
 }
 
 
+template <int W>
+hipError_t rec_lds_w(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s) {
+    if (bits != 16) return rec_lds_f<F8<W>>(logn, a, s);
+    return sub ? rec_lds_f<F16<W>, F16S<W>>(logn, a, s) : rec_lds_f<F16<W>>(logn, a, s);
+}
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s) {
-    if (bits != 16) return rec_lds_f<F8<kLdsW>>(logn, a, s);
-    return sub ? rec_lds_f<F16<kLdsW>, F16S<kLdsW>>(logn, a, s) : rec_lds_f<F16<kLdsW>>(logn, a, s);
+    const bool narrow = (a.S + 127) / 128 < kLdsMinGrid;
+    return narrow ? rec_lds_w<2>(bits, logn, sub, a, s) : rec_lds_w<4>(bits, logn, sub, a, s);
 }
 
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
-    return bits == 16 ? enc_lds_f<F16<kLdsW>>(logm, verify, a, s) : enc_lds_f<F8<kLdsW>>(logm, verify, a, s);
+    const bool narrow = (a.shard_size + 127) / 128 * (uint64_t)a.nstripes < kLdsMinGrid;
+    if (narrow) return bits == 16 ? enc_lds_f<F16<2>>(logm, verify, a, s) : enc_lds_f<F8<2>>(logm, verify, a, s);
+    return bits == 16 ? enc_lds_f<F16<4>>(logm, verify, a, s) : enc_lds_f<F8<4>>(logm, verify, a, s);
 }
 
 }  // namespace rs
