@@ -1164,7 +1164,9 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 // bytes), i.e. 32W bytes of each row per workgroup.  The launchers use
 // 128-byte tiles (W = 4), or 64-byte tiles (W = 2) when 128-byte tiles would
 // give fewer than kLdsMinGrid workgroups (C5's 32 KiB per-GPU byte range:
-// 57.0 -> 52.8 us; full-size C4 / C5 are faster at 128 bytes).
+// 57.0 -> 52.8 us; full-size C4 / C5 are faster at 128 bytes).  A GF(2^16)
+// tile must cover whole 64-byte blocks (low bytes [0,32), high bytes
+// [32,64)), so W = 1 (32-byte tiles) is invalid: the parity tests reject it.
 constexpr uint64_t kLdsMinGrid = 512;
 
 template <class F>
