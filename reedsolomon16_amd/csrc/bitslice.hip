@@ -34,6 +34,8 @@
 // 48 accumulator.  The XOR networks are written as in-place inline asm so the
 // compiler cannot rename their intermediates into fresh registers, and every
 // butterfly and chunk is a scheduling region of its own.
+#include <algorithm>
+#include <cstdlib>
 #include <utility>
 
 #include "bs_tables.h"
@@ -480,8 +482,395 @@ __global__ void __launch_bounds__(512, 2) k_encode_bs(BsArgs a) {
 #endif
 }
 
+// ============================================================================
+// Half-plane encode (k_encode_hp): subfield geometries (TW::SUB), two
+// independent 256-thread workgroups per CU.
+//
+// In subfield coordinates every twiddle acts as the same 8x8 GF(2) map on
+// both byte halves, so a lane can hold one half (8 bit-planes) of a 64-byte
+// block, and the half becomes a lane bit.  A workgroup owns a 2 KB tile (32
+// blocks) of every row of one stripe; lane l = (block l & 31, half l >> 5) in
+// every wave, 4 waves.  The only lane-varying quantities are the block and the
+// half, so every twiddle is wave-uniform:
+//
+//   chunk IFFT layers r0, r1, r2 (dist 1, 2, 4; leopard16.go:694-741): wave w
+//     holds rows 8w + j (j = 0..7) of its half.  Their twiddles depend on the
+//     row bits above the layer (r3, r4 = w), so the wave's role is w.
+//   -> one LDS exchange (64 KB image: row x plane quad x lane) ->
+//   chunk IFFT layers r3, r4 (dist 8, 16): wave w holds the cosets
+//     co = 2w + u (u = 0, 1; row bits r0..r2) of rows co + 8t; twiddles
+//     depend only on r4 (a register index), so every wave runs the same code.
+//     XOR-accumulate into A (same layout, 64 VGPRs).
+//   final FFT layers r4, r3 (fftDIT leopard16.go:618-657) in A's layout,
+//   -> one exchange -> layers r2, r1, r0 on rows 8w + j, store.
+//
+// Loads/stores need whole 64-byte blocks (the bit-plane transpose and the
+// coordinate change mix both halves): lane (b, h) loads rows 8w + 4h + i
+// (i = 0..3) of block b, transposes them, and one v_permlane32_swap per plane
+// pair moves the other half of each row to the partner lane (l ^ 32).
+//
+// One exchange per chunk (5 per tile), two barriers each, over 4 waves; the
+// second workgroup on the CU computes while this one waits.  Registers: 64
+// staged (next chunk, in flight) + 64 working + 64 accumulator.
+typedef uint32_t Half[8];
+
+// out ^= XOR of y[j] over the set bits j of mask (3-input XOR pairs).
+__device__ __forceinline__ void xor_net8(uint32_t &out, const Half &y, uint32_t mask) {
+    int pend = -1;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        if ((mask >> j) & 1) {
+            if (pend < 0) {
+                pend = j;
+            } else {
+                ixor3(out, y[pend], y[j]);
+                pend = -1;
+            }
+        }
+    }
+    if (pend >= 0) ixor(out, y[pend]);
+}
+__device__ __forceinline__ void xor8(Half &y, const Half &x) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) ixor(y[i], x[i]);
+}
+// x ^= y * twiddle (C >= 0: chunk C's IFFT slot; C < 0: FFT slot)
+template <class TW, int C, int SLOT>
+__device__ __forceinline__ void hp_mul_add(Half &x, const Half &y) {
+#ifdef RS_BS_ABL_NOMUL
+    return;
+#endif
+#pragma unroll
+    for (int i = 0; i < 8; i++) xor_net8(x[i], y, C < 0 ? TW::fft8[SLOT][i] : TW::ifft8[C < 0 ? 0 : C][SLOT][i]);
+}
+template <class TW, int C, int SLOT>
+__device__ __forceinline__ void hp_ifft2(Half &x, Half &y) {
+    xor8(y, x);
+    hp_mul_add<TW, C, SLOT>(x, y);
+    __builtin_amdgcn_sched_barrier(0);
+}
+template <class TW, int SLOT>
+__device__ __forceinline__ void hp_fft2(Half &x, Half &y) {
+    hp_mul_add<TW, -1, SLOT>(x, y);
+    xor8(y, x);
+    __builtin_amdgcn_sched_barrier(0);
+}
+// One byte half of bs_transpose (8 dwords <-> 8 planes).
+__device__ __forceinline__ void bs_transpose8(Half &w) {
+#ifdef RS_BS_ABL_NOTRANS
+    return;
+#endif
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const int s = 1 << k;
+        const uint32_t M = k == 0 ? 0x55555555u : k == 1 ? 0x33333333u : 0x0F0F0F0Fu;
+#pragma unroll
+        for (int a = 0; a < 8; a++)
+            if (!(a & s)) bs_xchg(w[a], w[a + s], s, M);
+    }
+}
+// Subfield coordinates of a whole row held as (lo planes, hi planes).
 template <class TW>
-hipError_t launch_bs_t(bool verify, const BsArgs &a, int grid, hipStream_t s) {
+__device__ __forceinline__ void hp_psi(Half &lo, const Half &hi) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) xor_net8(lo[r], hi, TW::dmat[r]);
+}
+// Rows i (lanes 0-31: lo half, lanes 32-63: hi half) <-> full rows: R[i] / R[4+i]
+// hold the lo / hi planes of full row i on each lane, or the half rows i and
+// 4 + i after the swap (an involution).
+// In-place inline asm: the builtin's two results land in fresh registers, and
+// 32 swaps in flight at once cost the kernel 64 VGPRs.  s_nop 1: two wait
+// states between a VALU write of an operand and the swap that reads it.
+__device__ __forceinline__ void hp_swap_halves(Half (&R)[8]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        asm volatile(
+            "s_nop 1\n\t"
+            "v_permlane32_swap_b32 %0, %8\n\tv_permlane32_swap_b32 %1, %9\n\t"
+            "v_permlane32_swap_b32 %2, %10\n\tv_permlane32_swap_b32 %3, %11\n\t"
+            "v_permlane32_swap_b32 %4, %12\n\tv_permlane32_swap_b32 %5, %13\n\t"
+            "v_permlane32_swap_b32 %6, %14\n\tv_permlane32_swap_b32 %7, %15"
+            : "+v"(R[i][0]), "+v"(R[i][1]), "+v"(R[i][2]), "+v"(R[i][3]), "+v"(R[i][4]), "+v"(R[i][5]),
+              "+v"(R[i][6]), "+v"(R[i][7]), "+v"(R[4 + i][0]), "+v"(R[4 + i][1]), "+v"(R[4 + i][2]),
+              "+v"(R[4 + i][3]), "+v"(R[4 + i][4]), "+v"(R[4 + i][5]), "+v"(R[4 + i][6]), "+v"(R[4 + i][7]));
+    }
+}
+
+// LDS image of the half-plane kernel: row r, plane quad qh of lane l at byte
+// r * 2048 + qh * 1024 + l * 16 (every ds_*_b128 wave access is 1 KB contiguous).
+__device__ __forceinline__ uint32_t hp_row_addr(uint32_t lbase, int row) {
+    uint32_t b = lbase;
+    asm volatile("" : "+v"(b));
+    return b + (uint32_t)row * 2048u;
+}
+__device__ __forceinline__ void hp_put(uint32_t lbase, int row, const Half &v) {
+#ifdef RS_BS_ABL_NOLDS
+    return;
+#endif
+    const uint32_t ra = hp_row_addr(lbase, row);
+    *(lds_u4 *)(uintptr_t)ra = u32x4{v[0], v[1], v[2], v[3]};
+    *(lds_u4 *)(uintptr_t)(ra + 1024) = u32x4{v[4], v[5], v[6], v[7]};
+}
+__device__ __forceinline__ void hp_get(uint32_t lbase, int row, Half &v) {
+#ifdef RS_BS_ABL_NOLDS
+#pragma unroll
+    for (int q = 0; q < 8; q++) asm volatile("" : "+v"(v[q]));
+    return;
+#endif
+    const uint32_t ra = hp_row_addr(lbase, row);
+    const u32x4 x = *(const lds_u4 *)(uintptr_t)ra;
+    const u32x4 y = *(const lds_u4 *)(uintptr_t)(ra + 1024);
+    v[0] = x[0], v[1] = x[1], v[2] = x[2], v[3] = x[3];
+    v[4] = y[0], v[5] = y[1], v[6] = y[2], v[7] = y[3];
+}
+
+template <class TW, bool VERIFY>
+struct HpEncoder {
+    static_assert(TW::SUB, "the half-plane kernel needs every twiddle in the GF(2^8) subfield");
+    static constexpr int NCH = TW::NCH;
+    static constexpr int TILE = 2048;  // column bytes per tile (32 blocks)
+    const BsArgs &a;
+    uint32_t lbase;  // this lane's LDS byte address of row 0, quad 0
+    int lane, w, h, blk;
+    Half St[8];  // staged full rows i: St[i] = dwords 0-7 (low bytes), St[4+i] = dwords 8-15
+    Half R[8];   // working rows
+    Half A[8];   // accumulator: coset u = 0, 1 (co = 2w + u), rows co + 8t at A[4u + t]
+
+    __device__ __forceinline__ void bar() { lds_barrier(); }
+
+    // Load rows 32c + 8w + 4h + i of `tile` through a buffer descriptor over
+    // the stripe's data rows: rows past k and bytes past the last row's end
+    // read as zero (range check), a tile past the end has an empty range.
+    // Lanes whose block lies past the row end read bytes of the next row;
+    // their results are never stored.
+    __device__ __forceinline__ void stage(int tile, int c) {
+        const int tps = a.tiles_per_stripe;
+        const int stripe = tile / tps, ct = tile - stripe * tps;
+        const bool live = tile < a.ntiles;
+#ifdef RS_BS_ABL_NOLOAD
+        const uint32_t range = 0;
+#else
+        const uint32_t range = live ? a.span : 0u;
+#endif
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.data + (live ? (uint64_t)stripe * a.stripe_stride : 0)), 0, (int)range, 0x00020000);
+        // lane part of the offset (block, half); opaque so that the compiler
+        // does not precompute every chunk's offsets
+        uint32_t voff = (uint32_t)ct * TILE + (uint32_t)blk * 64 + (uint32_t)(4 * h) * (uint32_t)a.row_stride;
+        asm volatile("" : "+v"(voff));
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            // wave-uniform row of the h = 0 lanes (rows >= k are out of range: zeros)
+            const uint32_t soff = (uint32_t)(32 * c + 8 * w + i) * (uint32_t)a.row_stride;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * 16, soff, 0);
+                uint32_t *d = q < 2 ? &St[i][q * 4] : &St[4 + i][(q - 2) * 4];
+                d[0] = x[0], d[1] = x[1], d[2] = x[2], d[3] = x[3];
+            }
+        }
+    }
+
+    // IFFT layers r0, r1, r2 on rows 8W + j (pass-0 slots 3g.., g = 2W + j/4;
+    // pass-1 slot 24 + 3 r4 + 2 r3 for layer r2).
+    template <int C, int W>
+    __device__ __forceinline__ void phase1() {
+        hp_ifft2<TW, C, 3 * (2 * W)>(R[0], R[1]);
+        hp_ifft2<TW, C, 3 * (2 * W) + 2>(R[2], R[3]);
+        hp_ifft2<TW, C, 3 * (2 * W + 1)>(R[4], R[5]);
+        hp_ifft2<TW, C, 3 * (2 * W + 1) + 2>(R[6], R[7]);
+        hp_ifft2<TW, C, 3 * (2 * W) + 1>(R[0], R[2]);
+        hp_ifft2<TW, C, 3 * (2 * W) + 1>(R[1], R[3]);
+        hp_ifft2<TW, C, 3 * (2 * W + 1) + 1>(R[4], R[6]);
+        hp_ifft2<TW, C, 3 * (2 * W + 1) + 1>(R[5], R[7]);
+        constexpr int s2 = 24 + 3 * (W >> 1) + ((W & 1) ? 2 : 0);
+        hp_ifft2<TW, C, s2>(R[0], R[4]);
+        hp_ifft2<TW, C, s2>(R[1], R[5]);
+        hp_ifft2<TW, C, s2>(R[2], R[6]);
+        hp_ifft2<TW, C, s2>(R[3], R[7]);
+    }
+
+    template <int C>
+    __device__ __forceinline__ void chunk(int tile) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int q = 0; q < 8; q++) R[i][q] = St[i][q];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            bs_transpose8(R[i]);
+            bs_transpose8(R[4 + i]);
+            hp_psi<TW>(R[i], R[4 + i]);
+        }
+        hp_swap_halves(R);
+        // consume the staged rows before the next chunk's loads are issued
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int q = 0; q < 8; q++) asm volatile("" : "+v"(R[i][q])::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (C + 1 < NCH) stage(tile, C + 1);
+        else stage(tile + (int)gridDim.x, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        dispatch<4>(w, [&](auto W) { phase1<C, decltype(W)::value>(); });
+        bar();  // every wave has read the previous image
+#pragma unroll
+        for (int j = 0; j < 8; j++) hp_put(lbase, 8 * w + j, R[j]);
+        bar();
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) hp_get(lbase, 2 * w + u + 8 * t, R[4 * u + t]);
+        // IFFT layers r3 (pass-1 m02: slot 25 for r4 = 0, 28 for r4 = 1) and r4 (slot 30)
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            hp_ifft2<TW, C, 25>(R[4 * u], R[4 * u + 1]);
+            hp_ifft2<TW, C, 28>(R[4 * u + 2], R[4 * u + 3]);
+            hp_ifft2<TW, C, 30>(R[4 * u], R[4 * u + 2]);
+            hp_ifft2<TW, C, 30>(R[4 * u + 1], R[4 * u + 3]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (C == 0) {
+#pragma unroll
+                for (int q = 0; q < 8; q++) A[j][q] = R[j][q];
+            } else {
+                xor8(A[j], R[j]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    template <int... Cs>
+    __device__ __forceinline__ void chunks(int tile, std::integer_sequence<int, Cs...>) {
+        (chunk<Cs>(tile), ...);
+    }
+
+    // FFT layers r2 (pass-1 m02), r1 (pass-1 m01/m23), r0 (pass-2 slot 15 + r/2) on rows 8W + j.
+    template <int W>
+    __device__ __forceinline__ void fft_b() {
+        constexpr int s0 = 3 + 3 * W;
+        hp_fft2<TW, s0 + 1>(R[0], R[4]);
+        hp_fft2<TW, s0 + 1>(R[1], R[5]);
+        hp_fft2<TW, s0 + 1>(R[2], R[6]);
+        hp_fft2<TW, s0 + 1>(R[3], R[7]);
+        hp_fft2<TW, s0>(R[0], R[2]);
+        hp_fft2<TW, s0>(R[1], R[3]);
+        hp_fft2<TW, s0 + 2>(R[4], R[6]);
+        hp_fft2<TW, s0 + 2>(R[5], R[7]);
+        hp_fft2<TW, 15 + 4 * W>(R[0], R[1]);
+        hp_fft2<TW, 16 + 4 * W>(R[2], R[3]);
+        hp_fft2<TW, 17 + 4 * W>(R[4], R[5]);
+        hp_fft2<TW, 18 + 4 * W>(R[6], R[7]);
+    }
+
+    __device__ __forceinline__ void run() {
+        int tile = blockIdx.x;
+        stage(tile, 0);
+        for (; tile < a.ntiles; tile += gridDim.x) {
+            chunks(tile, std::make_integer_sequence<int, NCH>{});
+            // FFT layers r4 (pass-0 m02, slot 1) and r3 (slot 0 for r4 = 0, 2 for r4 = 1) in A's layout
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                hp_fft2<TW, 1>(A[4 * u], A[4 * u + 2]);
+                hp_fft2<TW, 1>(A[4 * u + 1], A[4 * u + 3]);
+                hp_fft2<TW, 0>(A[4 * u], A[4 * u + 1]);
+                hp_fft2<TW, 2>(A[4 * u + 2], A[4 * u + 3]);
+            }
+            bar();
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+#pragma unroll
+                for (int t = 0; t < 4; t++) hp_put(lbase, 2 * w + u + 8 * t, A[4 * u + t]);
+            bar();
+#pragma unroll
+            for (int j = 0; j < 8; j++) hp_get(lbase, 8 * w + j, R[j]);
+            dispatch<4>(w, [&](auto W) { fft_b<decltype(W)::value>(); });
+            hp_swap_halves(R);
+            // parity rows 8w + 4h + i < p, through a descriptor over the stripe's
+            // parity rows (lanes past the row end store nothing: exec mask)
+            const int tps = a.tiles_per_stripe;
+            const int stripe = tile / tps, ct = tile - stripe * tps;
+            const uint32_t col = (uint32_t)ct * TILE + (uint32_t)blk * 64;
+            const __amdgpu_buffer_rsrc_t ps = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(a.parity + (uint64_t)stripe * a.stripe_stride), 0, (int)a.pspan, 0x00020000);
+            uint32_t voff = col + (uint32_t)(4 * h) * (uint32_t)a.row_stride;
+            asm volatile("" : "+v"(voff));
+            uint32_t bad = 0;
+            if (col < a.S) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int row = 8 * w + 4 * h + i;
+                    if (row >= TW::P) continue;
+                    hp_psi<TW>(R[i], R[4 + i]);
+                    bs_transpose8(R[i]);
+                    bs_transpose8(R[4 + i]);
+                    const uint32_t soff = (uint32_t)(8 * w + i) * (uint32_t)a.row_stride;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const int o = (k & 1) * 4;
+                        const u32x4 v = k < 2 ? u32x4{R[i][o], R[i][o + 1], R[i][o + 2], R[i][o + 3]}
+                                              : u32x4{R[4 + i][o], R[4 + i][o + 1], R[4 + i][o + 2], R[4 + i][o + 3]};
+                        if constexpr (VERIFY) {
+                            const u32x4 old = __builtin_amdgcn_raw_buffer_load_b128(ps, voff + k * 16, soff, 0);
+                            bad |= (old[0] ^ v[0]) | (old[1] ^ v[1]) | (old[2] ^ v[2]) | (old[3] ^ v[3]);
+                        } else {
+#ifdef RS_BS_NT_STORE
+                            __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * 16, soff, 2);
+#else
+                            __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * 16, soff, 0);
+#endif
+                        }
+                    }
+                }
+            }
+            if constexpr (VERIFY) {
+                const uint64_t m = __ballot(bad != 0);
+                if (m && lane == __ffsll((unsigned long long)m) - 1)
+                    __hip_atomic_store(a.mismatch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+};
+
+template <class TW, bool VERIFY>
+__global__ void __launch_bounds__(256, 2) k_encode_hp(BsArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[16 * 1024];  // 32 rows x 2 KB
+    HpEncoder<TW, VERIFY> e{a};
+    e.lane = threadIdx.x & 63;
+    e.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    e.h = e.lane >> 5;
+    e.blk = e.lane & 31;
+    e.lbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)lds + e.lane * 16;
+    e.run();
+}
+
+// RS_BS_KERNEL=1 selects the round-1 512-thread kernel for subfield
+// geometries too (A/B experiments only).
+bool hp_enabled() {
+    const char *e = getenv("RS_BS_KERNEL");
+    return !(e && e[0] == '1');
+}
+
+template <class TW>
+hipError_t launch_bs_t(bool verify, BsArgs a, int cus, hipStream_t s) {
+    if constexpr (TW::SUB) {
+        // buffer offsets are 32-bit: the data rows of one stripe must span < 4 GiB
+        if (hp_enabled() && (uint64_t)(a.k - 1) * a.row_stride + a.S < (1ull << 32)) {
+            a.tiles_per_stripe = (int)((a.S + 2047) / 2048);
+            a.ntiles = a.tiles_per_stripe * a.nstripes;
+            a.span = (uint32_t)((uint64_t)(a.k - 1) * a.row_stride + a.S);
+            a.pspan = (uint32_t)((uint64_t)(a.p - 1) * a.row_stride + a.S);
+            const int grid = std::min(a.ntiles, 2 * cus);
+            if (verify) hipLaunchKernelGGL((k_encode_hp<TW, true>), dim3(grid), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_encode_hp<TW, false>), dim3(grid), dim3(256), 0, s, a);
+            return hipGetLastError();
+        }
+    }
+    a.tiles_per_stripe = (int)((a.S + 4095) / 4096);
+    a.ntiles = a.tiles_per_stripe * a.nstripes;
+    const int grid = std::min(a.ntiles, cus);
     if (verify) hipLaunchKernelGGL((k_encode_bs<TW, true>), dim3(grid), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((k_encode_bs<TW, false>), dim3(grid), dim3(512), 0, s, a);
     return hipGetLastError();
@@ -497,9 +886,9 @@ bool encode_bs_available(int k, int p) {
     return false;
 }
 
-hipError_t launch_encode_bs(bool verify, const BsArgs &a, int grid, hipStream_t s) {
+hipError_t launch_encode_bs(bool verify, const BsArgs &a, int cus, hipStream_t s) {
 #define RS_BS_LAUNCH(K, P) \
-    if (a.k == K && a.p == P) return launch_bs_t<BsTw<K, P>>(verify, a, grid, s);
+    if (a.k == K && a.p == P) return launch_bs_t<BsTw<K, P>>(verify, a, cus, s);
     RS_BS_CONFIGS(RS_BS_LAUNCH)
 #undef RS_BS_LAUNCH
     return hipErrorNotSupported;

@@ -389,11 +389,9 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
             b.k = c->k;
             b.p = c->p;
             b.nstripes = nstripes;
-            b.tiles_per_stripe = (int)((S + 4095) / 4096);
-            b.ntiles = b.tiles_per_stripe * nstripes;
             b.mismatch = mismatch;
             if (!c->cus) HIP_TRY(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
-            HIP_TRY(launch_encode_bs(mismatch != nullptr, b, std::min(b.ntiles, c->cus), s));
+            HIP_TRY(launch_encode_bs(mismatch != nullptr, b, c->cus, s));
             return RS_OK;
         }
         // split kernel: strided rows whose data span fits a 32-bit buffer offset

@@ -90,10 +90,13 @@ struct BsArgs {
     const uint8_t *data;    // stripe 0, data row 0
     uint8_t *parity;        // stripe 0, parity row 0
     uint64_t row_stride, stripe_stride, S;
-    int k, p, nstripes, tiles_per_stripe, ntiles;  // tile = 4 KB of every row of one stripe
+    int k, p, nstripes;
+    int tiles_per_stripe, ntiles;  // set by the launcher (tile width depends on the kernel)
+    uint32_t span, pspan;          // set by the launcher: (k-1)*row_stride + S, (p-1)*row_stride + S
     int *mismatch;          // verify
 };
 bool encode_bs_available(int k, int p);
-hipError_t launch_encode_bs(bool verify, const BsArgs &a, int grid, hipStream_t s);
+// cus: compute units of the device (the launcher sizes its persistent grid).
+hipError_t launch_encode_bs(bool verify, const BsArgs &a, int cus, hipStream_t s);
 
 }  // namespace rs

@@ -7,7 +7,10 @@ built from, no device calls:
 * the twiddle matrices tools/gen_bs_tables.cpp writes into build/bs_tables.h,
   applied as GF(2) matrices in the kernel's pass and butterfly order (chunk
   IFFT passes 1-3, XOR-accumulate, FFT passes A-C), give the oracle's parity
-  bit for bit (leopard16.go:128-224) for every geometry compiled in.
+  bit for bit (leopard16.go:128-224) for every geometry compiled in;
+* the same for the half-plane kernel's order (k_encode_hp: IFFT layers
+  r0-r2 per 8-row group, layers r3-r4 per coset, FFT layers r4-r3 per coset,
+  r2-r0 per group) and its slot indexing.
 """
 import os
 import re
@@ -180,6 +183,82 @@ def test_subfield_tables_match_oracle():
         blk = data.reshape(k, -1, 64)
         sym = (blk[:, :, :32].astype(np.uint32) | (blk[:, :, 32:].astype(np.uint32) << 8)).reshape(k, -1)
         par = to_sub(dmat, bs_encode(tabs, k, p, to_sub(dmat, sym))).reshape(p, -1, 32)
+        got = np.concatenate([(par & 0xFF).astype(np.uint8), (par >> 8).astype(np.uint8)], axis=2).reshape(p, S)
+        assert np.array_equal(got, orc.encode(16, k, p, data)), (k, p)
+    assert n >= 1
+
+
+def hp_encode(tabs, k, p, sym):
+    """k_encode_hp's butterfly order and twiddle slots (bitslice.hip HpEncoder)."""
+    ifft, fft = tabs[0], tabs[1]
+
+    def i2(X, a, b, M):
+        X[b] ^= X[a]
+        X[a] ^= gf2_apply(M, X[b])
+
+    def f2(X, a, b, M):
+        X[a] ^= gf2_apply(M, X[b])
+        X[b] ^= X[a]
+
+    acc = None
+    for c in range(ifft.shape[0]):
+        X = np.zeros((32, sym.shape[1]), np.uint32)
+        n = min(32, k - 32 * c)
+        X[:n] = sym[32 * c:32 * c + n]
+        T = ifft[c]
+        for w in range(4):  # phase 1: rows 8w + j, layers r0, r1, r2
+            b = 8 * w
+            for j in (0, 2, 4, 6):
+                i2(X, b + j, b + j + 1, T[3 * (2 * w + (j >> 2)) + (2 if j & 2 else 0)])
+            for j in (0, 1, 4, 5):
+                i2(X, b + j, b + j + 2, T[3 * (2 * w + (j >> 2)) + 1])
+            for j in range(4):
+                i2(X, b + j, b + j + 4, T[24 + 3 * (w >> 1) + (2 if w & 1 else 0)])
+        for co in range(8):  # phase 2: rows co + 8t, layers r3, r4
+            r = [co + 8 * t for t in range(4)]
+            i2(X, r[0], r[1], T[25])
+            i2(X, r[2], r[3], T[28])
+            i2(X, r[0], r[2], T[30])
+            i2(X, r[1], r[3], T[30])
+        acc = X if acc is None else acc ^ X
+    for co in range(8):  # FFT layers r4, r3 per coset
+        r = [co + 8 * t for t in range(4)]
+        f2(acc, r[0], r[2], fft[1])
+        f2(acc, r[1], r[3], fft[1])
+        f2(acc, r[0], r[1], fft[0])
+        f2(acc, r[2], r[3], fft[2])
+    for w in range(4):  # FFT layers r2, r1, r0 per group
+        b, s0 = 8 * w, 3 + 3 * w
+        for j in range(4):
+            f2(acc, b + j, b + j + 4, fft[s0 + 1])
+        f2(acc, b, b + 2, fft[s0])
+        f2(acc, b + 1, b + 3, fft[s0])
+        f2(acc, b + 4, b + 6, fft[s0 + 2])
+        f2(acc, b + 5, b + 7, fft[s0 + 2])
+        for j in (0, 2, 4, 6):
+            f2(acc, b + j, b + j + 1, fft[15 + 4 * w + (j >> 1)])
+    return acc[:p]
+
+
+def test_half_plane_schedule_matches_oracle():
+    """k_encode_hp's order in subfield coordinates (the only mode it runs in)."""
+    n = 0
+    for (k, p), (_, _, sub) in load_tables().items():
+        if sub is None:
+            continue
+        n += 1
+        dmat, i8, f8 = sub
+
+        def widen(t):
+            return (t | (t << np.uint32(8)))[..., list(range(8)) * 2] & np.concatenate(
+                [np.full(8, 0xFF, np.uint32), np.full(8, 0xFF00, np.uint32)])
+        tabs = (widen(i8), widen(f8))
+        rng = np.random.default_rng(3 * k + p)
+        S = 128
+        data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+        blk = data.reshape(k, -1, 64)
+        sym = (blk[:, :, :32].astype(np.uint32) | (blk[:, :, 32:].astype(np.uint32) << 8)).reshape(k, -1)
+        par = to_sub(dmat, hp_encode(tabs, k, p, to_sub(dmat, sym))).reshape(p, -1, 32)
         got = np.concatenate([(par & 0xFF).astype(np.uint8), (par >> 8).astype(np.uint8)], axis=2).reshape(p, S)
         assert np.array_equal(got, orc.encode(16, k, p, data)), (k, p)
     assert n >= 1

@@ -27,10 +27,18 @@ def test_bs_path_selected(k, p):
     assert rs.New16(k, p).encode_path == "bs16-m32"
 
 
+@pytest.fixture(params=["hp", "bs"])
+def kernel(request, monkeypatch):
+    """Both bit-sliced kernels: the half-plane kernel (default for subfield
+    geometries) and the round-1 512-thread kernel (RS_BS_KERNEL=1)."""
+    monkeypatch.setenv("RS_BS_KERNEL", "2" if request.param == "hp" else "1")
+    return request.param
+
+
 @pytest.mark.parametrize("k,p,S,n", [(128, 32, 64, 1), (128, 32, 4096 * 3 + 64 * 5, 1), (128, 32, 8192, 3),
                                      (32, 32, 64 * 37, 2), (32, 32, 4096 * 64, 5), (100, 17, 4096 * 3 + 320, 2),
-                                     (100, 17, 4096, 5)])
-def test_bs_batch_matches_oracle(torch, k, p, S, n):
+                                     (100, 17, 4096, 5), (128, 32, 2048 * 700 + 64 * 3, 2)])
+def test_bs_batch_matches_oracle(torch, kernel, k, p, S, n):
     rng = np.random.default_rng(k * 131 + p * 7 + S + n)
     datas = [rng.integers(0, 256, (k, S), dtype=np.uint8) for _ in range(n)]
     slab = torch.zeros((n, k + p, S), dtype=torch.uint8, device="cuda")
