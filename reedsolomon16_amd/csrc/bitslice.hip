@@ -816,7 +816,9 @@ struct HpEncoder {
                             const u32x4 old = __builtin_amdgcn_raw_buffer_load_b128(ps, voff + k * 16, soff, 0);
                             bad |= (old[0] ^ v[0]) | (old[1] ^ v[1]) | (old[2] ^ v[2]) | (old[3] ^ v[3]);
                         } else {
-#ifdef RS_BS_NT_STORE
+#if defined(RS_BS_ABL_NOSTORE)
+                            asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+#elif defined(RS_BS_NT_STORE)
                             __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * 16, soff, 2);
 #else
                             __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * 16, soff, 0);

@@ -109,7 +109,14 @@ struct rs_codec {
     int n = 0, logn = 0;
     DevBuf<uint32_t> dtw_ifft, dtw_fft;
 
-    // scratch
+    // scratch shared by the codec's calls (row table, multi-pass work rows,
+    // reconstruct blob).  Calls may run on different caller streams and the
+    // device-resident encodes return before their kernels finish, so every call
+    // records scratch_ev after its last launch, and the next call orders itself
+    // behind it (stream wait) before touching the scratch (host wait before a
+    // host-side overwrite or a reallocation).
+    hipEvent_t scratch_ev = nullptr;
+    bool scratch_used = false;
     DevBuf<uint8_t> work;
     DevBuf<uint8_t *> rows;         // row-pointer table (non-strided inputs)
     std::vector<uint8_t *> rows_host;
@@ -143,6 +150,10 @@ struct rs_codec {
         if (!dev_ready && !stream) return;
         DeviceGuard g(device);
         if (stream) (void)hipStreamSynchronize(stream);
+        if (scratch_ev) {
+            (void)hipEventSynchronize(scratch_ev);
+            (void)hipEventDestroy(scratch_ev);
+        }
         tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); dtw_ifft.release(); dtw_fft.release();
         work.release(); rows.release();
         if (hflag) (void)hipHostFree(hflag);
@@ -304,8 +315,37 @@ int build_decode_plan(rs_codec *c) {
 
 hipStream_t pick_stream(rs_codec *c, void *s) { return s ? (hipStream_t)s : c->stream; }
 
-// Data rows [0,k) and parity rows [k,k+p) as RowSets: strided when the
-// pointers are equally spaced (AllocAligned slab), else via a device table.
+// Order this call's stream behind the previous user of the codec scratch.
+int scratch_acquire(rs_codec *c, hipStream_t s) {
+    if (c->scratch_used) HIP_TRY(hipStreamWaitEvent(s, c->scratch_ev, 0));
+    return RS_OK;
+}
+// Host wait for the previous user of the scratch (before a host-side write or a reallocation).
+int scratch_host_wait(rs_codec *c) {
+    if (c->scratch_used) HIP_TRY(hipEventSynchronize(c->scratch_ev));
+    return RS_OK;
+}
+// Mark the scratch as used by the work queued on `s` so far.
+int scratch_release(rs_codec *c, hipStream_t s) {
+    if (!c->scratch_ev) HIP_TRY(hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->scratch_ev, s));
+    c->scratch_used = true;
+    return RS_OK;
+}
+// DevBuf::ensure for codec scratch: a reallocation frees a buffer that a
+// kernel of an earlier call (on another stream) may still read.
+template <class T>
+int scratch_ensure(rs_codec *c, DevBuf<T> &b, size_t want) {
+    if (want <= b.n) return RS_OK;
+    if (int e = scratch_host_wait(c)) return e;
+    HIP_TRY(b.ensure(want));
+    return RS_OK;
+}
+
+// Data rows [0,k) and parity rows [k,k+p) as RowSets: strided when both sets'
+// pointers are equally spaced (AllocAligned slab), else both via a device
+// table (one strided set and one table would reach a kernel whose TABLE
+// parameter covers both: a null table dereference).
 int make_rowsets(rs_codec *c, uint8_t *const *d, hipStream_t s, RowSet &data, RowSet &par) {
     auto strided = [&](int lo, int cnt, RowSet &rs) {
         if (cnt == 1) { rs = RowSet{nullptr, d[lo], 0}; return true; }
@@ -320,13 +360,18 @@ int make_rowsets(rs_codec *c, uint8_t *const *d, hipStream_t s, RowSet &data, Ro
     if (ok_d && ok_p) return RS_OK;
     std::vector<uint8_t *> tbl(d, d + c->total);
     if (tbl != c->rows_host || c->rows.n < (size_t)c->total) {
-        HIP_TRY(hipStreamSynchronize(s));  // previous users of the table are done
-        HIP_TRY(c->rows.ensure(c->total));
+        // previous users of the table are done: this call's stream and the last
+        // scratch user (a device-resident encode may still run on another stream)
+        HIP_TRY(hipStreamSynchronize(s));
+        if (int e = scratch_host_wait(c)) return e;
+        if (int e = scratch_ensure(c, c->rows, c->total)) return e;
         HIP_TRY(hipMemcpy(c->rows.p, tbl.data(), c->total * sizeof(uint8_t *), hipMemcpyHostToDevice));
         c->rows_host = tbl;
     }
-    if (!ok_d) data = RowSet{c->rows.p, nullptr, 0};
-    if (!ok_p) par = RowSet{c->rows.p + c->k, nullptr, 0};
+    // both sets from the table: the kernels take one layout (template TABLE)
+    // for data and parity rows alike
+    data = RowSet{c->rows.p, nullptr, 0};
+    par = RowSet{c->rows.p + c->k, nullptr, 0};
     return RS_OK;
 }
 
@@ -345,7 +390,7 @@ int run_passes(rs_codec *c, bool inverse, uint8_t *work, uint64_t S, int logsz, 
 
 int encode_multipass(rs_codec *c, RowSet data, RowSet par, uint64_t S, int *mismatch, hipStream_t s) {
     const int m = c->m;
-    HIP_TRY(c->work.ensure((size_t)2 * m * S));
+    if (int e = scratch_ensure(c, c->work, (size_t)2 * m * S)) return e;
     uint8_t *acc = c->work.p, *tmp = c->work.p + (size_t)m * S;
     const int is = ifft_slots(c->logm);
     for (int ch = 0; ch < c->nchunks; ch++) {
@@ -525,7 +570,7 @@ int upload_reconstruct(rs_codec *c, const RecPlan &pl, const std::vector<uint8_t
     const size_t s_in = pl.tw_in.size() * 4, s_out = pl.tw_out.size() * 4, s_pos = std::max<size_t>(pl.pos.size(), 1) * 4;
     const size_t o_dst = al(s_src), o_in = o_dst + al(s_dst), o_out = o_in + al(s_in), o_pos = o_out + al(s_out);
     const size_t total = o_pos + al(s_pos);
-    HIP_TRY(c->rc_blob.ensure(total));
+    if (int e = scratch_ensure(c, c->rc_blob, total)) return e;
     if (c->rc_host_n < total) {
         if (c->rc_host) HIP_TRY(hipHostFree(c->rc_host));
         c->rc_host = nullptr;
@@ -572,7 +617,7 @@ int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipS
         HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
         return RS_OK;
     }
-    HIP_TRY(c->work.ensure((size_t)n * S));
+    if (int e = scratch_ensure(c, c->work, (size_t)n * S)) return e;
     uint8_t *w = c->work.p;
     HIP_TRY(launch_scale_in(c->bits, w, S, c->rc_src + (size_t)set * n, c->rc_tw_in, n, s));
     int e = run_passes(c, true, w, S, c->logn, c->m + c->k, c->dtw_ifft.p, s);
@@ -590,9 +635,13 @@ int reconstruct_device(rs_codec *c, uint8_t *const *d, const std::vector<uint8_t
     RecPlan pl;
     int e = plan_reconstruct(c, present, recover_all, pl);
     if (e) return e;
+    e = scratch_acquire(c, s);
+    if (e) return e;
     e = upload_reconstruct(c, pl, {d}, s);
     if (e) return e;
     e = launch_reconstruct(c, pl, 0, S, s);
+    if (e) return e;
+    e = scratch_release(c, s);
     if (e) return e;
     HIP_TRY(hipStreamSynchronize(s));  // the pinned staging of the upload is reused by the next call
     return RS_OK;
@@ -686,11 +735,26 @@ bool is_pageable(const void *p) {
     return at.type != hipMemoryTypeHost && at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeManaged;
 }
 
+// Drains the pipeline's three streams on every return path: on an error exit
+// copies into or out of the caller's rows (or the bounce slab) may still be in
+// flight, and the next call reuses the staging slabs.
+struct PipeDrain {
+    rs_codec *c;
+    ~PipeDrain() {
+        if (c->s_in) (void)hipStreamSynchronize(c->s_in);
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        if (c->s_out) (void)hipStreamSynchronize(c->s_out);
+    }
+};
+
 int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, const std::vector<uint8_t> &present,
                   bool recover_all, int *ok) {
     int e = ensure_host_pipe(c);
     if (e) return e;
+    PipeDrain drain_guard{c};
     hipStream_t sc = c->stream;
+    e = scratch_acquire(c, sc);
+    if (e) return e;
     const int k = c->k, total = c->total;
     std::vector<int> in_rows, out_rows;
     RecPlan pl;
@@ -709,8 +773,9 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     const uint64_t slab = (uint64_t)total * seg;
     HIP_TRY(c->stage.ensure((size_t)kHostBufs * slab));
     // scratch of the multi-pass paths, sized before any launch (no realloc mid-pipeline)
-    if (op == HostOp::Reconstruct) HIP_TRY(c->work.ensure((size_t)c->n * seg));
-    else if (c->logm > kMaxRegLogM) HIP_TRY(c->work.ensure((size_t)2 * c->m * seg));
+    if (op == HostOp::Reconstruct) e = scratch_ensure(c, c->work, (size_t)c->n * seg);
+    else if (c->logm > kMaxRegLogM) e = scratch_ensure(c, c->work, (size_t)2 * c->m * seg);
+    if (e) return e;
     // outputs in pageable memory go D2H into a pinned bounce slab, and the host
     // copies segment j - 1 out while the device works on segment j
     bool use_bounce = false;
@@ -782,6 +847,8 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
         }
     }
     if (op == HostOp::Verify) HIP_TRY(hipMemcpyAsync(c->hflag, c->dflag, sizeof(int), hipMemcpyDeviceToHost, sc));
+    e = scratch_release(c, sc);
+    if (e) return e;
     if (use_bounce && nseg) {
         e = drain(nseg - 1);
         if (e) return e;
@@ -995,7 +1062,11 @@ int rs_encode_dev(rs_codec *c, uint8_t *const *d, size_t S, void *stream) {
     RowSet data, par;
     int e = make_rowsets(c, d, s, data, par);
     if (e) return e;
+    e = scratch_acquire(c, s);
+    if (e) return e;
     e = encode_device(c, data, par, S, 0, 1, nullptr, s);
+    if (e) return e;
+    e = scratch_release(c, s);
     if (e) return e;
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return RS_OK;
@@ -1011,7 +1082,11 @@ int rs_encode_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size_t st
     if (int ie = ensure_device(c)) return ie;
     hipStream_t s = pick_stream(c, stream);
     RowSet data{nullptr, base, row_stride}, par{nullptr, base + (size_t)c->k * row_stride, row_stride};
-    int e = encode_device(c, data, par, S, stripe_stride, nstripes, nullptr, s);
+    int e = scratch_acquire(c, s);
+    if (e) return e;
+    e = encode_device(c, data, par, S, stripe_stride, nstripes, nullptr, s);
+    if (e) return e;
+    e = scratch_release(c, s);
     if (e) return e;
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return RS_OK;
@@ -1031,8 +1106,12 @@ int rs_verify_dev(rs_codec *c, uint8_t *const *d, size_t S, int *ok, void *strea
     RowSet data, par;
     int e = make_rowsets(c, d, s, data, par);
     if (e) return e;
+    e = scratch_acquire(c, s);
+    if (e) return e;
     HIP_TRY(hipMemsetAsync(c->dflag, 0, sizeof(int), s));
     e = encode_device(c, data, par, S, 0, 1, c->dflag, s);
+    if (e) return e;
+    e = scratch_release(c, s);
     if (e) return e;
     HIP_TRY(hipMemcpyAsync(c->hflag, c->dflag, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));

@@ -1149,7 +1149,7 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 
 
 // ---------------------------------------------------------------- LDS-resident transforms (n <= 256)
-// One workgroup owns a 128-byte tile (two 64-byte blocks) of every row and
+// One workgroup owns a 32W-byte tile (W = 4: two 64-byte blocks) of every row and
 // keeps all n rows of it in LDS for the whole operation, so HBM sees each
 // input row once and each output row once (the multi-pass path above re-reads
 // the n-row work slab on every radix-4 layer).  Used for reconstruct
@@ -1169,8 +1169,22 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 // [32,64)), so W = 1 (32-byte tiles) is invalid: the parity tests reject it.
 constexpr uint64_t kLdsMinGrid = 512;
 
+// RS_UNIT_WIDTH=wide / narrow forces the per-launch unit-width choices below
+// (LDS tiles of 128 vs 64 bytes; GF(2^8) register units of 16 vs 4 bytes) so
+// the parity tests cover every variant at small sizes.  Testing only.
+int unit_width_override() {
+    const char *e = getenv("RS_UNIT_WIDTH");
+    if (!e) return -1;
+    return e[0] == 'n' ? 1 : e[0] == 'w' ? 0 : -1;
+}
+bool pick_narrow(bool automatic) {
+    const int o = unit_width_override();
+    return o < 0 ? automatic : o == 1;
+}
+
 template <class F>
 struct LTile {
+    static_assert(!F::SYM16 || F::W >= 2, "a GF(2^16) LDS tile must cover whole 64-byte blocks (W >= 2)");
     static constexpr bool W16 = F::SYM16;
     static constexpr int TB = 32 * F::W;                  // bytes of each row owned by a workgroup
     static constexpr int ROW = TB + 16;                   // LDS row stride (144 B at TB = 128 spreads rows over the banks)
@@ -1285,7 +1299,7 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
     }
 }
 
-// Reconstruct (leopard16.go:432-568) of one stripe, one 128-byte tile per workgroup.
+// Reconstruct (leopard16.go:432-568) of one stripe, one 32W-byte tile (LTile) per workgroup.
 // F scales rows in and out (full-field tables); FT runs the transforms (F, or
 // F16S when every transform twiddle lies in GF(2^8)).
 template <class F, class FT, int LOGN>
@@ -1467,7 +1481,7 @@ hipError_t launch_encode_reg(int bits, int logm, bool verify, const EncodeArgs &
 #ifndef RS_F8_NARROW
 #define RS_F8_NARROW 1
 #endif
-        const bool narrow = RS_F8_NARROW && (a.shard_size / 16 + 255) / 256 * (uint64_t)a.nstripes < 1024;
+        const bool narrow = pick_narrow(RS_F8_NARROW && (a.shard_size / 16 + 255) / 256 * (uint64_t)a.nstripes < 1024);
         switch (logm) {
             case 0: return enc_reg<F8<4>, 0>(verify, a, s);
             case 1: return enc_reg<F8<4>, 1>(verify, a, s);
@@ -1588,12 +1602,12 @@ hipError_t rec_lds_w(int bits, int logn, bool sub, const RecArgs &a, hipStream_t
     return sub ? rec_lds_f<F16<W>, F16S<W>>(logn, a, s) : rec_lds_f<F16<W>>(logn, a, s);
 }
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s) {
-    const bool narrow = (a.S + 127) / 128 < kLdsMinGrid;
+    const bool narrow = pick_narrow((a.S + 127) / 128 < kLdsMinGrid);
     return narrow ? rec_lds_w<2>(bits, logn, sub, a, s) : rec_lds_w<4>(bits, logn, sub, a, s);
 }
 
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
-    const bool narrow = (a.shard_size + 127) / 128 * (uint64_t)a.nstripes < kLdsMinGrid;
+    const bool narrow = pick_narrow((a.shard_size + 127) / 128 * (uint64_t)a.nstripes < kLdsMinGrid);
     if (narrow) return bits == 16 ? enc_lds_f<F16<2>>(logm, verify, a, s) : enc_lds_f<F8<2>>(logm, verify, a, s);
     return bits == 16 ? enc_lds_f<F16<4>>(logm, verify, a, s) : enc_lds_f<F8<4>>(logm, verify, a, s);
 }

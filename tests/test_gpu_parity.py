@@ -419,3 +419,86 @@ def test_host_reconstruct_c4_output_memory(outputs):
     for i in er:
         assert lens[i] == S
         assert np.array_equal(outs[i], full[i]), i
+
+
+# Codec scratch shared across caller streams: device-resident encodes return
+# before their kernels finish, so a second call on another stream must not
+# overwrite the row-pointer table (non-strided rows) or the multi-pass work
+# rows (m > 256) the first call's kernels are still reading.
+@pytest.mark.parametrize("bits,k,p,S,layout", [(16, 128, 32, 1 << 16, "table"), (8, 10, 4, 1 << 18, "table"),
+                                               (16, 300, 300, 1 << 12, "slab")])
+def test_device_encode_two_streams(torch_dev, bits, k, p, S, layout):
+    torch = torch_dev
+    rng = np.random.default_rng(k + p + S)
+    datas = [rand_data(rng, k, S) for _ in range(2)]
+    c = rs.ReedSolomon(k, p, bits)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for j in range(2):
+        if layout == "table":
+            rows = [torch.from_numpy(datas[j][i].copy()).cuda() for i in range(k)] + \
+                   [torch.zeros(S, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        else:
+            rows = torch.zeros((k + p, S), dtype=torch.uint8, device="cuda")
+            rows[:k] = torch.from_numpy(datas[j]).cuda()
+        outs.append(rows)
+    torch.cuda.synchronize()
+    for j in range(2):  # back to back, no synchronization in between
+        c.encode_dev(outs[j], stream=streams[j])
+    torch.cuda.synchronize()
+    for j in range(2):
+        got = np.stack([r.cpu().numpy() for r in outs[j][k:]])
+        assert np.array_equal(got, orc.encode(bits, k, p, datas[j])), f"stream {j}"
+
+
+# Unit-width variants (RS_UNIT_WIDTH forces the per-launch choice): the
+# 64-byte and 128-byte LDS tiles of the LDS-resident encode / reconstruct
+# (both fields, both coordinate systems), and the 4- and 16-byte GF(2^8)
+# register units, at sizes the oracle finishes in seconds.
+@pytest.mark.parametrize("width", ["narrow", "wide"])
+@pytest.mark.parametrize("bits,k,p,S", [(8, 10, 4, 4096), (8, 100, 28, 4096 + 192), (16, 100, 28, 4096 + 192),
+                                        (16, 70, 40, 2048), (8, 70, 40, 2048), (16, 128, 32, 4096 + 640)])
+def test_unit_width_variants(monkeypatch, width, bits, k, p, S):
+    monkeypatch.setenv("RS_UNIT_WIDTH", width)
+    monkeypatch.setenv("RS_BS", "0")
+    rng = np.random.default_rng(k + p + S + bits)
+    data = rand_data(rng, k, S)
+    ref = orc.encode(bits, k, p, data)
+    c = rs.ReedSolomon(k, p, bits)
+    shards = [np.ascontiguousarray(data[i]) for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+    c.encode(shards)
+    assert np.array_equal(np.stack(shards[k:]), ref), c.encode_path
+    full = [data[i] for i in range(k)] + [ref[i] for i in range(p)]
+    for nosub in (["0", "1"] if bits == 16 else ["0"]):
+        monkeypatch.setenv("RS_NO_SUB", nosub)
+        c2 = rs.ReedSolomon(k, p, bits)
+        er = set(rng.choice(k + p, p, replace=False).tolist())
+        sh = [None if i in er else full[i].copy() for i in range(k + p)]
+        c2.reconstruct(sh)
+        for i in range(k + p):
+            assert np.array_equal(sh[i], full[i]), (nosub, i)
+
+
+@pytest.mark.parametrize("strided", ["data", "parity"])
+def test_device_encode_mixed_layout(torch_dev, strided):
+    """One row set equally spaced (a slab), the other scattered (rows of a
+    buffer in permuted order): both must go through the row table (round 1
+    passed a null table for the strided set)."""
+    torch = torch_dev
+    k, p, S = 16, 8, 4096
+    rng = np.random.default_rng(7)
+    data = rand_data(rng, k, S)
+    ref = orc.encode(16, k, p, data)
+    c = rs.New16(k, p)
+    slab = torch.zeros((k + p, S), dtype=torch.uint8, device="cuda")
+    slab[:k] = torch.from_numpy(data).cuda()
+    rows = list(slab)
+    lo, n = (k, p) if strided == "data" else (0, k)
+    perm = np.r_[1, 0, 2:n][rng.permutation(n)] if n > 2 else np.arange(n)[::-1]
+    scat = torch.zeros((n, S), dtype=torch.uint8, device="cuda")
+    scat[torch.from_numpy(perm).cuda()] = slab[lo:lo + n]
+    for i in range(n):
+        rows[lo + i] = scat[int(perm[i])]
+    c.encode_dev(rows)
+    torch.cuda.synchronize()
+    assert np.array_equal(np.stack([r.cpu().numpy() for r in rows[k:]]), ref)
