@@ -1,17 +1,28 @@
-"""Headline benchmark: device-resident GF(2^16) encode, 128 data + 32 parity x 1 MiB
-shards (BASELINE.json configs[2] / C3), --stripes stripes (default 16) per rank per step.
+"""Headline benchmark: device-resident GF(2^16) encode (BASELINE.json metric),
+128 data + 32 parity x 1 MiB shards (configs[2] / C3) by default, or
+1024 + 256 x 256 KiB (configs[4] / C5) with --workload C5.
 
-A step is one encode of B synthetic C3 stripes already resident in HBM, all in
-one kernel launch (rs_encode_dev_batch; the stripes are independent objects,
-as a storage server encodes many at once).  Multi-GPU: one process per GPU, each rank encodes its own
-stripe (independent objects, no collective on the data path) -> weak scaling;
-value = data bytes encoded by all ranks / max-over-ranks wall time.
+A step encodes B synthetic stripes (--stripes, default 16) already resident in
+HBM, in one kernel launch per rank (rs_encode_dev_batch).
+
+Multi-GPU (one process per GPU, launched by torch.distributed.run):
+  --split bytes   (default) the north-star layout: rank r owns the byte range
+                  dist.byte_range(S, r, N) of every shard of the same B stripes
+                  (column independence, leopard16.go:778-792) and encodes it;
+                  no collective on the data path.  Total work is fixed as N
+                  grows -> "scaling": "strong"; value = B*k*S data bytes /
+                  max-over-ranks wall time.
+  --split stripes each rank encodes B stripes of its own -> "weak".
 
 Prints one JSON line (rank 0).  `roofline` is for the dominant (only) kernel:
-achieved = algorithmic bytes per launch ((k+p)*S: read k rows, write p rows)
-/ its mean duration: one HIP event pair on the launch stream around the K
-back-to-back launches of the timed region, divided by K.  `cpu_baseline` times the oracle's scalar C
-restatement of the reference path (single thread) on a bounded sample.
+achieved = algorithmic bytes per launch ((k+p)*bytes-per-row: read k rows,
+write p rows) / its mean duration (one HIP event pair on the launch stream
+around the timed launches, divided by their count).  `single_stripe` repeats
+the kernel timing with one stripe per launch (the reference's Encode
+granularity).  `cpu_baseline` times the reference-equivalent AVX2 port of the
+encode (oracle/leopard_ref.c, test/bench infrastructure) on a bounded sample:
+1 thread (the reference is single-threaded per call) and N threads over byte
+ranges.
 """
 import argparse
 import json
@@ -22,42 +33,63 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-K, P, S = 128, 32, 1 << 20
+WORKLOADS = {"C3": (128, 32, 1 << 20), "C5": (1024, 256, 256 << 10)}
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(seconds: float):
-    """Oracle (scalar C restatement of the reference Ref path), 1 thread, same config."""
+def cpu_baseline(K, P, S, seconds: float, threads: int):
+    """Reference-equivalent AVX2 port (oracle/leopard_ref.c orc16_encode_simd),
+    same geometry, one stripe per call; scalar Ref oracle if AVX2 is absent."""
     import numpy as np
 
     from oracle import orc
 
     rng = np.random.default_rng(0x5EED)
     data = rng.integers(0, 256, (K, S), dtype=np.uint8)
-    orc.encode(16, K, P, data)  # warm (table init)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        orc.encode(16, K, P, data)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {
-        "value": round(n * K * S / el / 2**30, 4),
-        "unit": "GiB/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"{n} encodes of one 128+32 x 1 MiB stripe (oracle/leopard_ref.c scalar Ref path, -O2), {el:.1f} s",
-    }
+    par = np.zeros((P, S), np.uint8)
+    simd = orc.simd_available()
+
+    def run(th):
+        if simd:
+            orc.encode_simd(K, P, data, th, par)
+        else:
+            orc.encode(16, K, P, data)
+
+    def rate(th, budget):
+        run(th)  # warm (tables, page faults)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            run(th)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return n, el
+
+    n1, el1 = rate(1, seconds / 2)
+    out = {"value": None, "unit": "GiB/s", "cores": 1, "kind": "port",
+           "single_thread": round(n1 * K * S / el1 / 2**30, 4)}
+    if simd and threads > 1:
+        nN, elN = rate(threads, seconds / 2)
+        out["value"] = round(nN * K * S / elN / 2**30, 4)
+        out["cores"] = threads
+        out["sample"] = (f"{K}+{P} x {S >> 10} KiB stripe, AVX2 nibble-table port of the reference encode "
+                         f"(oracle/leopard_ref.c, -O3): {n1} encodes on 1 thread in {el1:.1f} s, "
+                         f"{nN} encodes on {threads} threads (byte ranges) in {elN:.1f} s")
+    else:
+        out["value"] = out["single_thread"]
+        out["sample"] = (f"{K}+{P} x {S >> 10} KiB stripe, {'AVX2 port' if simd else 'scalar Ref oracle'}, "
+                         f"{n1} encodes on 1 thread in {el1:.1f} s")
+    return out
 
 
-def load_traffic(kernel_name: str):
+def load_traffic(kernel_name: str, workload: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kernel_name, {}).get("hbm_bytes_per_launch")
+        e = d.get(f"{workload}:{kernel_name}") or (d.get(kernel_name) if workload == "C3" else None)
+        return (e or {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -67,16 +99,21 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="C3")
+    ap.add_argument("--split", choices=["bytes", "stripes"], default="bytes",
+                    help="multi-GPU layout: byte ranges of the same stripes (strong) or own stripes (weak)")
+    ap.add_argument("--stripes", type=int, default=16, help="stripes encoded per step (one launch per rank)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--stripes", type=int, default=16,
-                    help="stripes encoded per step (one launch); each is 128+32 x 1 MiB")
+    ap.add_argument("--no-single", action="store_true", help="skip the one-stripe-per-launch figure")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
     import reedsolomon16_amd as rs
+    from reedsolomon16_amd import dist as rsd
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -88,11 +125,18 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
+    K, P, S = WORKLOADS[args.workload]
+    B = args.stripes
+    if args.split == "bytes":
+        lo, hi = rsd.byte_range(S, rank, world)
+    else:
+        lo, hi = 0, S
+    W = hi - lo  # bytes of each row this rank holds and encodes
     codec = rs.New16(K, P, device=dev.index)
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED + rank)
-    B = args.stripes
-    slab = torch.randint(0, 256, (B, K + P, S), dtype=torch.uint8, device=dev, generator=g)
+    # this rank's resident bytes: B stripes x (k+p) rows x W bytes (its byte range)
+    slab = torch.randint(0, 256, (B, K + P, W), dtype=torch.uint8, device=dev, generator=g)
     stream = torch.cuda.current_stream()
 
     def barrier():
@@ -100,39 +144,47 @@ def main():
             dist.barrier(device_ids=[dev.index])
         torch.cuda.synchronize()
 
+    def timed(view, steps):
+        """Wall time of `steps` launches and their mean kernel time from HIP
+        events on the launch stream (one pair around all of them)."""
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        barrier()
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(steps):
+            codec.encode_dev_batch(view, stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        barrier()
+        return el, e0.elapsed_time(e1) / steps
+
     for _ in range(args.warmup):
         codec.encode_dev_batch(slab, stream)
-    barrier()
+    el, kern_ms = timed(slab, args.steps)
+    one_ms = None
+    if not args.no_single:
+        for _ in range(10):
+            codec.encode_dev_batch(slab[:1], stream)
+        _, one_ms = timed(slab[:1], max(50, args.steps))
 
-    # One HIP event pair on the launch stream brackets the K back-to-back
-    # launches: per-launch event pairs would insert their own gaps.
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier()
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(args.steps):
-        codec.encode_dev_batch(slab, stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    barrier()
-    kern_ms = e0.elapsed_time(e1) / args.steps
-
-    t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([el, kern_ms, one_ms or 0.0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el, kern_ms = float(t[0]), float(t[1])
+    el, kern_ms, one_ms = float(t[0]), float(t[1]), float(t[2]) or None
 
     ms_per_step = el / args.steps * 1e3
-    data_bytes = world * args.steps * B * K * S
+    job_stripes = B if args.split == "bytes" else world * B
+    data_bytes = args.steps * job_stripes * K * S
     value = data_bytes / el / 2**30
-    alg_bytes = B * (K + P) * S
+    alg_bytes = B * (K + P) * W  # per launch on one rank
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     kname = codec.encode_path
 
     if rank == 0:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         res = {
-            "metric": "encode GiB/s (device-resident), 128+32 x 1 MiB shards",
+            "metric": "encode GiB/s (device-resident), %d+%d x %d KiB shards" % (K, P, S >> 10),
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -140,31 +192,38 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.split == "bytes" else "weak",
             "vs_baseline": None,
             "dtype": "u8 (GF(2^16) symbols)",
             "data": "synthetic (uniform random bytes, torch.randint seed 0x5EED+rank)",
             "config": {
-                "workload": f"GF(2^16) Leopard encode, 128 data + 32 parity shards x 1 MiB, {B} stripes per rank per step (one launch)",
+                "workload": f"{args.workload}: GF(2^16) Leopard encode, {K} data + {P} parity shards x {S >> 10} KiB, "
+                            f"{B} stripes per step (one launch per rank)",
                 "stripes_per_step": B,
                 "data_shards": K,
                 "parity_shards": P,
                 "shard_bytes": S,
-                "parallelism": f"independent stripes, {world} rank(s)",
+                "parallelism": (f"byte-range split over {world} rank(s): {W} bytes of every row per rank"
+                                if args.split == "bytes" else f"independent stripes, {world} rank(s)"),
                 "kernel_path": kname,
             },
             "hbm_gib_s": round(world * args.steps * alg_bytes / el / 2**30, 2),
+            "per_rank_kernel_ms": round(kern_ms, 5),
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
-                "traffic": load_traffic(kname),
+                "traffic": load_traffic(kname, args.workload) if (world == 1 and B == 16) else None,
                 "kernel_ms": round(kern_ms, 5),
                 "alg_bytes_per_launch": alg_bytes,
             },
-            "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(args.cpu_seconds),
+            "single_stripe": None if one_ms is None else {
+                "kernel_ms": round(one_ms, 5),
+                "frac": round((K + P) * W / (one_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+            },
+            "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(K, P, S, args.cpu_seconds, threads),
         }
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -86,6 +86,25 @@ int rs_encode_idx(rs_codec *codec, const uint8_t *data_shard, size_t len, int id
 int rs_update(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards,
               uint8_t *const *new_data, const size_t *new_lens, int nnew);
 
+/* ---------------- Split / Join (leopard16.go:232-340) ---------------- */
+/* Shard size Split would produce for `len` bytes of data: ceil(len/k) rounded
+ * up to 64 (leopard16.go:283-288; len when total == 1 and len % 64 == 0).
+ * RS_ERR_SHORT_DATA for len == 0. */
+int rs_split_shard_size(const rs_codec *codec, size_t len, size_t *per_shard);
+/* Split (leopard16.go:277-340) into a caller slab: shard i is written at
+ * dst + i*dst_stride (per_shard bytes): data rows get the data, the rest of
+ * the last one and every parity row are zeroed (the reference's padding).
+ * data and dst may each be host memory (pageable or pinned) or device memory
+ * (HBM), so the data can land directly in the device slab the encode reads;
+ * device copies run on `stream` (NULL: the codec's stream, synchronous). */
+int rs_split(rs_codec *codec, const uint8_t *data, size_t len, uint8_t *dst, size_t dst_stride, void *stream);
+/* Join (leopard16.go:231-269): the first out_size bytes of the data shards,
+ * in order, into dst.  ErrTooFewShards / ErrReconstructRequired (a missing
+ * data shard: lens[i] == 0) / ErrShortData as the reference.  Shards and dst
+ * may be host or device memory. */
+int rs_join(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards, uint8_t *dst,
+            size_t out_size, void *stream);
+
 /* ---------------- Host-resident pipeline controls ---------------- */
 /* rs_encode / rs_verify / rs_reconstruct stream the stripe through the GPU in
  * column segments (H2D, kernel and D2H on three streams, 3 staging slabs).

@@ -46,6 +46,8 @@ def lib():
         L.orc8_mul.argtypes = [C.c_void_p, C.c_void_p, C.c_uint8, C.c_size_t]
         L.orc8_mul_log.argtypes = [C.c_uint8, C.c_uint8]
         L.orc8_mul_log.restype = C.c_uint8
+        L.orc16_encode_simd.argtypes = [C.c_int, C.c_int, P(C.c_void_p), C.c_size_t, C.c_int]
+        L.orc16_simd_available.restype = C.c_int
         if L.orc_init() != 0:
             raise MemoryError("oracle table init failed")
         _lib = L
@@ -150,3 +152,20 @@ def encode(bits: int, k: int, p: int, data: np.ndarray) -> np.ndarray:
     if e != 0:
         raise RuntimeError(f"oracle encode error {e}")
     return np.stack(shards[k:])
+
+
+def simd_available() -> bool:
+    return bool(lib().orc16_simd_available())
+
+
+def encode_simd(k: int, p: int, data: np.ndarray, threads: int = 1, parity: np.ndarray = None) -> np.ndarray:
+    """GF(2^16) encode with the reference-equivalent AVX2 port (leopard_ref.c,
+    CPU baseline only): data (k,S) uint8 -> parity (p,S); `threads` byte ranges."""
+    S = data.shape[1]
+    if parity is None:
+        parity = np.zeros((p, S), np.uint8)
+    arr = (C.c_void_p * (k + p))(*([data[i].ctypes.data for i in range(k)] + [parity[i].ctypes.data for i in range(p)]))
+    e = lib().orc16_encode_simd(k, p, arr, S, threads)
+    if e != 0:
+        raise RuntimeError(f"simd encode error {e}")
+    return parity

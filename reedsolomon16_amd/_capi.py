@@ -39,6 +39,9 @@ def lib() -> C.CDLL:
     L.rs_reconstruct_dev.argtypes = [vp, P(vp), P(C.c_uint8), sz, i32, vp]
     L.rs_encode_dev_batch.argtypes = [vp, vp, sz, sz, i32, sz, vp]
     L.rs_set_host_segment.argtypes = [vp, sz]
+    L.rs_split_shard_size.argtypes = [vp, sz, P(sz)]
+    L.rs_split.argtypes = [vp, vp, sz, vp, sz, vp]
+    L.rs_join.argtypes = [vp, P(vp), P(sz), i32, vp, sz, vp]
     L.rs_host_alloc.argtypes = [sz, P(vp)]
     L.rs_host_free.argtypes = [vp]
     L.rs_host_free.restype = None

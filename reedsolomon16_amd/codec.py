@@ -281,41 +281,90 @@ class ReedSolomon:
         """Update (leopard16.go:273-275): not supported."""
         _check(self._L.rs_update(self._h, None, None, 0, None, None, 0))
 
-    # ---------------- Split / Join (leopard16.go:232-340): host byte layout either side of the codec
+    # ---------------- Split / Join (leopard16.go:232-340) through the C-ABI (rs_split / rs_join)
+    def split_shard_size(self, length: int) -> int:
+        """Bytes per shard Split produces for `length` bytes (leopard16.go:283-288)."""
+        per = C.c_size_t(0)
+        _check(self._L.rs_split_shard_size(self._h, length, C.byref(per)))
+        return per.value
+
     def split(self, data) -> list:
+        """Split (leopard16.go:277-340): k+p equal shards of one 64-byte-aligned
+        host slab; data rows carry the data, the padding and parity rows are zero."""
         data = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        data = np.ascontiguousarray(data, dtype=np.uint8)
         if len(data) == 0:
             raise ErrShortData("not enough data to fill the number of requested shards")
-        k, total = self.data_shards(), self.total_shards()
+        per = self.split_shard_size(len(data))
+        total = self.total_shards()
         if total == 1 and len(data) & 63 == 0:
             return [data]
-        per = (len(data) + k - 1) // k
-        per = (per + 63) // 64 * 64
-        buf = np.zeros(total * per, dtype=np.uint8)
-        buf[:len(data)] = data
-        return [buf[i * per:(i + 1) * per] for i in range(total)]
+        raw = np.empty(per * total + 64, dtype=np.uint8)
+        off = (-raw.ctypes.data) % 64
+        slab = raw[off:off + per * total]
+        _check(self._L.rs_split(self._h, data.ctypes.data, len(data), slab.ctypes.data, per, None))
+        return [slab[i * per:(i + 1) * per] for i in range(total)]
+
+    def split_dev(self, data, out=None, stream=None):
+        """Split into a device slab: returns a [k+p, per_shard] uint8 CUDA tensor
+        (or fills `out`, rows contiguous); `data` is host bytes/ndarray or a
+        device tensor.  The shards land in HBM in the layout encode_dev reads."""
+        import torch
+
+        if isinstance(data, torch.Tensor):
+            src, n = data.data_ptr(), data.numel()
+            keep = data
+        else:
+            keep = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray)
+                                        else data, dtype=np.uint8)
+            src, n = keep.ctypes.data, keep.nbytes
+        if n == 0:
+            raise ErrShortData("not enough data to fill the number of requested shards")
+        per = self.split_shard_size(n)
+        if out is None:
+            out = torch.empty((self.total_shards(), per), dtype=torch.uint8, device="cuda")
+        _check(self._L.rs_split(self._h, src, n, out.data_ptr(), out.stride(0), _stream_handle(stream)))
+        if stream is None:
+            torch.cuda.current_stream().synchronize()
+        del keep
+        return out
 
     def join(self, dst, shards: list, out_size: int) -> None:
+        """Join (leopard16.go:231-269): write the first out_size data bytes to dst
+        (a file-like object with .write)."""
         k = self.data_shards()
         if len(shards) < k:
             raise ErrTooFewShards("too few shards given")
-        shards = shards[:k]
-        size = 0
-        for s in shards:
-            if s is None:
-                raise ErrReconstructRequired("reconstruction required as one or more required data shards are nil")
-            size += len(s)
-            if size >= out_size:
-                break
-        if size < out_size:
-            raise ErrShortData("not enough data to fill the number of requested shards")
-        write = out_size
-        for s in shards:
-            if write < len(s):
-                dst.write(bytes(np.asarray(s)[:write]))
-                return
-            dst.write(bytes(np.asarray(s)))
-            write -= len(s)
+        ptrs = (C.c_void_p * k)()
+        lens = (C.c_size_t * k)()
+        keep = []
+        for i in range(k):
+            s = shards[i]
+            if s is None or len(s) == 0:
+                ptrs[i], lens[i] = None, 0
+                continue
+            a = np.ascontiguousarray(s, dtype=np.uint8)
+            keep.append(a)
+            ptrs[i], lens[i] = a.ctypes.data, a.nbytes
+        out = np.empty(out_size, dtype=np.uint8)
+        _check(self._L.rs_join(self._h, ptrs, lens, k, out.ctypes.data if out_size else None, out_size, None))
+        dst.write(out.tobytes())
+
+    def join_dev(self, rows, out_size: int) -> np.ndarray:
+        """Join from device-resident shards (a [k+p, S] tensor or a list): the
+        first out_size bytes as a host array (device -> host copies)."""
+        k = self.data_shards()
+        if hasattr(rows, "dim"):
+            ptrs = (C.c_void_p * k)(*[rows[i].data_ptr() for i in range(k)])
+            lens = (C.c_size_t * k)(*([rows.shape[1]] * k))
+        else:
+            if len(rows) < k:
+                raise ErrTooFewShards("too few shards given")
+            ptrs = (C.c_void_p * k)(*[None if r is None else r.data_ptr() for r in rows[:k]])
+            lens = (C.c_size_t * k)(*[0 if r is None else r.numel() for r in rows[:k]])
+        out = np.empty(out_size, dtype=np.uint8)
+        _check(self._L.rs_join(self._h, ptrs, lens, k, out.ctypes.data if out_size else None, out_size, None))
+        return out
 
     # ---------------- device-resident operations (torch CUDA tensors)
     def encode_dev(self, rows, stream=None) -> None:
@@ -336,11 +385,16 @@ class ReedSolomon:
         _check(self._L.rs_reconstruct_dev(self._h, ptrs, pr, S, int(recover_all), _stream_handle(stream)))
 
     def encode_dev_batch(self, slab, stream=None) -> None:
-        """Encode a [nstripes, k+p, S] uint8 CUDA tensor (one launch for all stripes)."""
-        if slab.dim() != 3 or slab.shape[1] != self.total_shards() or not slab.is_contiguous():
-            raise TypeError("slab must be a contiguous [nstripes, k+p, S] uint8 CUDA tensor")
+        """Encode a [nstripes, k+p, S] uint8 CUDA tensor in one launch.  Any
+        view whose rows are contiguous works (stride(2) == 1): stripe and row
+        strides come from the tensor, so a byte-range slice slab[:, :, lo:hi]
+        of a resident slab is encoded in place."""
+        if slab.dim() != 3 or slab.shape[1] != self.total_shards():
+            raise TypeError("slab must be a [nstripes, k+p, S] uint8 CUDA tensor")
+        if not slab.is_cuda or slab.dtype.itemsize != 1 or slab.stride(2) != 1:
+            raise TypeError("slab rows must be contiguous uint8 on a CUDA device")
         n, _, S = slab.shape
-        _check(self._L.rs_encode_dev_batch(self._h, slab.data_ptr(), S, slab.stride(0), n, S,
+        _check(self._L.rs_encode_dev_batch(self._h, slab.data_ptr(), slab.stride(1), slab.stride(0), n, S,
                                            _stream_handle(stream)))
 
 

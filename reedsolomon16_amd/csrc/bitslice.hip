@@ -513,6 +513,9 @@ __global__ void __launch_bounds__(512, 2) k_encode_bs(BsArgs a) {
 // second workgroup on the CU computes while this one waits.  Registers: 64
 // staged (next chunk, in flight) + 64 working + 64 accumulator.
 typedef uint32_t Half[8];
+#ifndef RS_HP_LOAD_AUX
+#define RS_HP_LOAD_AUX 0     // cache policy of the data loads (2 = nt)
+#endif
 
 // out ^= XOR of y[j] over the set bits j of mask (3-input XOR pairs).
 __device__ __forceinline__ void xor_net8(uint32_t &out, const Half &y, uint32_t mask) {
@@ -643,6 +646,7 @@ struct HpEncoder {
     // read as zero (range check), a tile past the end has an empty range.
     // Lanes whose block lies past the row end read bytes of the next row;
     // their results are never stored.
+    template <int I0, int I1>
     __device__ __forceinline__ void stage(int tile, int c) {
         const int tps = a.tiles_per_stripe;
         const int stripe = tile / tps, ct = tile - stripe * tps;
@@ -659,7 +663,7 @@ struct HpEncoder {
         uint32_t voff = (uint32_t)ct * TILE + (uint32_t)blk * 64 + (uint32_t)(4 * h) * (uint32_t)a.row_stride;
         asm volatile("" : "+v"(voff));
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = I0; i < I1; i++) {
             // wave-uniform row of the h = 0 lanes (rows >= k are out of range: zeros)
             const uint32_t soff = (uint32_t)(32 * c + 8 * w + i) * (uint32_t)a.row_stride;
 #pragma unroll
@@ -690,6 +694,19 @@ struct HpEncoder {
         hp_ifft2<TW, C, s2>(R[3], R[7]);
     }
 
+    // Next chunk's rows i in [I0, I1): chunk C + 1 of this tile, or chunk 0 of the next tile.
+    template <int C, int I0, int I1>
+    __device__ __forceinline__ void prefetch(int tile) {
+        if (C + 1 < NCH) stage<I0, I1>(tile, C + 1);
+        else stage<I0, I1>(tile + (int)gridDim.x, 0);
+    }
+
+    // The next chunk's loads go out in two halves so that at most 160 of the
+    // 256 VGPRs hold data (A 64 + R 64 + half of St during the transposes and
+    // layers r0-r2; A 64 + St 64 + one coset's 32 during layers r3-r4): rows
+    // i = 0, 1 once the staged rows are transposed, rows 2, 3 once the
+    // phase-1 rows are in the LDS image.  (Issuing all of them at the chunk
+    // start, with 192 VGPRs of data live, spilled to scratch: +8 % HBM traffic.)
     template <int C>
     __device__ __forceinline__ void chunk(int tile) {
         __builtin_amdgcn_sched_barrier(0);
@@ -704,42 +721,42 @@ struct HpEncoder {
             hp_psi<TW>(R[i], R[4 + i]);
         }
         hp_swap_halves(R);
-        // consume the staged rows before the next chunk's loads are issued
+        // consume the staged rows before their registers are reloaded
 #pragma unroll
         for (int i = 0; i < 8; i++)
 #pragma unroll
             for (int q = 0; q < 8; q++) asm volatile("" : "+v"(R[i][q])::"memory");
         __builtin_amdgcn_sched_barrier(0);
-        if (C + 1 < NCH) stage(tile, C + 1);
-        else stage(tile + (int)gridDim.x, 0);
+        prefetch<C, 0, 2>(tile);
         __builtin_amdgcn_sched_barrier(0);
         dispatch<4>(w, [&](auto W) { phase1<C, decltype(W)::value>(); });
         bar();  // every wave has read the previous image
 #pragma unroll
         for (int j = 0; j < 8; j++) hp_put(lbase, 8 * w + j, R[j]);
         bar();
-#pragma unroll
-        for (int u = 0; u < 2; u++)
-#pragma unroll
-            for (int t = 0; t < 4; t++) hp_get(lbase, 2 * w + u + 8 * t, R[4 * u + t]);
-        // IFFT layers r3 (pass-1 m02: slot 25 for r4 = 0, 28 for r4 = 1) and r4 (slot 30)
+        prefetch<C, 2, 4>(tile);
+        __builtin_amdgcn_sched_barrier(0);
+        // IFFT layers r3 (pass-1 m02: slot 25 for r4 = 0, 28 for r4 = 1) and r4
+        // (slot 30), one coset u (rows 2w + u + 8t) at a time
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            hp_ifft2<TW, C, 25>(R[4 * u], R[4 * u + 1]);
-            hp_ifft2<TW, C, 28>(R[4 * u + 2], R[4 * u + 3]);
-            hp_ifft2<TW, C, 30>(R[4 * u], R[4 * u + 2]);
-            hp_ifft2<TW, C, 30>(R[4 * u + 1], R[4 * u + 3]);
-        }
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if (C == 0) {
+            for (int t = 0; t < 4; t++) hp_get(lbase, 2 * w + u + 8 * t, R[t]);
+            hp_ifft2<TW, C, 25>(R[0], R[1]);
+            hp_ifft2<TW, C, 28>(R[2], R[3]);
+            hp_ifft2<TW, C, 30>(R[0], R[2]);
+            hp_ifft2<TW, C, 30>(R[1], R[3]);
 #pragma unroll
-                for (int q = 0; q < 8; q++) A[j][q] = R[j][q];
-            } else {
-                xor8(A[j], R[j]);
+            for (int t = 0; t < 4; t++) {
+                if (C == 0) {
+#pragma unroll
+                    for (int q = 0; q < 8; q++) A[4 * u + t][q] = R[t][q];
+                } else {
+                    xor8(A[4 * u + t], R[t]);
+                }
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
     }
 
     template <int... Cs>
@@ -767,7 +784,7 @@ struct HpEncoder {
 
     __device__ __forceinline__ void run() {
         int tile = blockIdx.x;
-        stage(tile, 0);
+        stage<0, 4>(tile, 0);
         for (; tile < a.ntiles; tile += gridDim.x) {
             chunks(tile, std::make_integer_sequence<int, NCH>{});
             // FFT layers r4 (pass-0 m02, slot 1) and r3 (slot 0 for r4 = 0, 2 for r4 = 1) in A's layout

@@ -747,6 +747,25 @@ struct PipeDrain {
     }
 };
 
+
+// Pointer kind for Split/Join: host memory (pageable, pinned or unknown to
+// HIP) is copied with memcpy, device memory with hipMemcpy*Async.
+bool is_device_ptr(const void *p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice;
+}
+
+// Split's shard size (leopard16.go:283-288): ceil(len / k) rounded up to 64.
+size_t split_per_shard(const rs_codec *c, size_t len) {
+    if (c->total == 1 && (len & 63) == 0) return len;
+    size_t per = (len + (size_t)c->k - 1) / (size_t)c->k;
+    return (per + 63) / 64 * 64;
+}
+
 int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, const std::vector<uint8_t> &present,
                   bool recover_all, int *ok) {
     int e = ensure_host_pipe(c);
@@ -1202,6 +1221,86 @@ int rs_reconstruct(rs_codec *c, uint8_t *const *shards, size_t *lens, int nshard
     if (e) return e;
     for (int i = 0; i < end; i++)
         if (!pr[i]) lens[i] = S;
+    return RS_OK;
+}
+
+int rs_split_shard_size(const rs_codec *c, size_t len, size_t *per_shard) {
+    if (!c || !per_shard) return RS_ERR_INVALID_ARG;
+    if (len == 0) return RS_ERR_SHORT_DATA;
+    *per_shard = split_per_shard(c, len);
+    return RS_OK;
+}
+
+int rs_split(rs_codec *c, const uint8_t *data, size_t len, uint8_t *dst, size_t dst_stride, void *stream) {
+    if (!c || !data || !dst) return RS_ERR_INVALID_ARG;
+    if (len == 0) return RS_ERR_SHORT_DATA;  // leopard16.go:279-281
+    const size_t per = split_per_shard(c, len);
+    if (dst_stride < per && c->total > 1) return RS_ERR_INVALID_ARG;
+    const int total = c->total;
+    const size_t nfull = std::min<size_t>(len / per, (size_t)total), rem = nfull < (size_t)total ? len - nfull * per : 0;
+    const bool ddev = is_device_ptr(dst), sdev = is_device_ptr(data);
+    if (!ddev && !sdev) {  // host -> host: plain copies, no device involved
+        for (int i = 0; i < total; i++) {
+            uint8_t *row = dst + (size_t)i * dst_stride;
+            const size_t have = (size_t)i < nfull ? per : (size_t)i == nfull ? rem : 0;
+            if (have) std::memcpy(row, data + (size_t)i * per, have);
+            if (have < per) std::memset(row + have, 0, per - have);
+        }
+        return RS_OK;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (int ie = ensure_device(c)) return ie;
+    hipStream_t s = pick_stream(c, stream);
+    if (nfull) HIP_TRY(hipMemcpy2DAsync(dst, dst_stride, data, per, per, nfull, hipMemcpyDefault, s));
+    if (rem) HIP_TRY(hipMemcpyAsync(dst + nfull * dst_stride, data + nfull * per, rem, hipMemcpyDefault, s));
+    const size_t zrow = nfull + (rem ? 1 : 0);
+    if (ddev) {
+        if (rem) HIP_TRY(hipMemsetAsync(dst + nfull * dst_stride + rem, 0, per - rem, s));
+        if (zrow < (size_t)total) HIP_TRY(hipMemset2DAsync(dst + zrow * dst_stride, dst_stride, 0, per, total - zrow, s));
+    } else {
+        HIP_TRY(hipStreamSynchronize(s));
+        if (rem) std::memset(dst + nfull * dst_stride + rem, 0, per - rem);
+        for (size_t i = zrow; i < (size_t)total; i++) std::memset(dst + i * dst_stride, 0, per);
+    }
+    if (!stream) HIP_TRY(hipStreamSynchronize(s));
+    return RS_OK;
+}
+
+int rs_join(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshards, uint8_t *dst, size_t out_size,
+            void *stream) {
+    if (!c || !shards || !lens || (!dst && out_size)) return RS_ERR_INVALID_ARG;
+    if (nshards < c->k) return RS_ERR_TOO_FEW_SHARDS;  // leopard16.go:232-236
+    size_t size = 0;
+    int use = 0;
+    for (int i = 0; i < c->k; i++) {  // :239-250
+        if (!shards[i] || lens[i] == 0) return RS_ERR_RECONSTRUCT_REQUIRED;
+        size += lens[i];
+        use = i + 1;
+        if (size >= out_size) break;
+    }
+    if (size < out_size) return RS_ERR_SHORT_DATA;  // :251-253
+    bool dev = is_device_ptr(dst);
+    for (int i = 0; i < use && !dev; i++) dev = is_device_ptr(shards[i]);
+    size_t written = 0;
+    if (!dev) {
+        for (int i = 0; i < use && written < out_size; i++) {  // :256-268
+            const size_t n = std::min(lens[i], out_size - written);
+            std::memcpy(dst + written, shards[i], n);
+            written += n;
+        }
+        return RS_OK;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (int ie = ensure_device(c)) return ie;
+    hipStream_t s = pick_stream(c, stream);
+    for (int i = 0; i < use && written < out_size; i++) {
+        const size_t n = std::min(lens[i], out_size - written);
+        HIP_TRY(hipMemcpyAsync(dst + written, shards[i], n, hipMemcpyDefault, s));
+        written += n;
+    }
+    if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return RS_OK;
 }
 

@@ -70,19 +70,34 @@ def verify_sharded(rows, rank: int, world: int, verify_fn: Callable, group=None,
 
 
 def gpu_encode_fn(codec, stream=None):
-    """Per-rank encode through the engine (device-resident slice rows)."""
+    """Per-rank encode through the engine: the [k+p, hi-lo] slice view goes to
+    the C-ABI as base + row stride (no per-row host objects)."""
     def fn(loc):
-        codec.encode_dev([loc[i] for i in range(loc.shape[0])], stream)
+        codec.encode_dev(loc, stream)
     return fn
 
 
 def gpu_verify_fn(codec, stream=None):
     def fn(loc):
-        return codec.verify_dev([loc[i] for i in range(loc.shape[0])], stream)
+        return codec.verify_dev(loc, stream)
     return fn
 
 
 def gpu_reconstruct_fn(codec, recover_all: bool = True, stream=None):
     def fn(loc, present):
-        codec.reconstruct_dev([loc[i] for i in range(loc.shape[0])], present, recover_all, stream)
+        codec.reconstruct_dev(loc, present, recover_all, stream)
     return fn
+
+
+def local_stripes(slab, rank: int, world: int):
+    """Column slice [lo, hi) of every row of every stripe of a [n, k+p, S] slab (a view)."""
+    lo, hi = byte_range(slab.shape[2], rank, world)
+    return slab[:, :, lo:hi]
+
+
+def encode_sharded_batch(slab, rank: int, world: int, codec, stream=None) -> None:
+    """Encode this rank's byte range of n stripes in one launch
+    (rs_encode_dev_batch over the strided view; no collective)."""
+    loc = local_stripes(slab, rank, world)
+    if loc.shape[2]:
+        codec.encode_dev_batch(loc, stream)

@@ -251,3 +251,26 @@ def test_subfield_coordinates():
         assert np.array_equal(back, F.mul_log(x, log_m)), e
     assert L.rs_debug_sub_twiddle(65535, t.ctypes.data) == 0 and not t[:5].any()
     assert L.rs_debug_sub_twiddle(int(F._log[300]), t.ctypes.data) == -1
+
+
+@pytest.mark.parametrize("k,p,n", [(4, 2, 1), (4, 2, 63), (4, 2, 256), (4, 2, 1025), (10, 4, 64 * 10), (10, 4, 64 * 10 + 1),
+                                   (128, 32, 1 << 16), (3, 1, 7)])
+def test_split_c_abi_matches_go_model(k, p, n):
+    """rs_split (host slab) against a transcription of leopard16.go:277-340:
+    perShard = roundup64(ceil(n / k)); data rows hold the bytes, then zeros;
+    parity rows zero."""
+    c = rs.New16(k, p)
+    data = np.random.default_rng(n + k).integers(0, 256, n, dtype=np.uint8)
+    per = -(-n // k)
+    per = -(-per // 64) * 64
+    assert c.split_shard_size(n) == per
+    want = np.zeros((k + p) * per, np.uint8)
+    want[:n] = data
+    got = c.split(data)
+    assert len(got) == k + p and all(len(s) == per for s in got)
+    assert np.array_equal(np.concatenate(got), want)
+    import io
+
+    buf = io.BytesIO()
+    c.join(buf, got, n)
+    assert buf.getvalue() == data.tobytes()

@@ -502,3 +502,27 @@ def test_device_encode_mixed_layout(torch_dev, strided):
     c.encode_dev(rows)
     torch.cuda.synchronize()
     assert np.array_equal(np.stack([r.cpu().numpy() for r in rows[k:]]), ref)
+
+
+@pytest.mark.parametrize("k,p,n", [(128, 32, (1 << 20) * 128 - 5), (10, 4, 1000), (4, 2, 64)])
+def test_split_into_device_slab_encode_join(torch_dev, k, p, n):
+    """rs_split straight into an HBM slab (host bytes -> device rows, padding and
+    parity rows zeroed on the device), encode_dev on it, rs_join back (device
+    rows -> host): the data round-trips and the parity is the oracle's."""
+    torch = torch_dev
+    c = rs.New16(k, p)
+    data = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8)
+    slab = c.split_dev(data)
+    per = c.split_shard_size(n)
+    assert slab.shape == (k + p, per)
+    host = c.split(data)
+    assert np.array_equal(slab.cpu().numpy(), np.stack(host))
+    c.encode_dev(slab)
+    torch.cuda.synchronize()
+    if k * per <= (16 << 20):
+        assert np.array_equal(slab[k:].cpu().numpy(), orc.encode(16, k, p, np.stack(host[:k])))
+    assert np.array_equal(c.join_dev(slab, n), data)
+    # device -> device split (data already in HBM)
+    dd = torch.from_numpy(data).cuda()
+    slab2 = c.split_dev(dd)
+    assert torch.equal(slab2[:k], slab[:k])

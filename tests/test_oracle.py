@@ -178,3 +178,14 @@ def test_golden_fixtures(name):
         sh = [None if er[i] else full[i].copy() for i in range(k + p)]
         e, got = orc.Oracle(bits, k, p).reconstruct(sh, True)
         assert e == 0 and all(np.array_equal(got[i], full[i]) for i in range(k + p))
+
+
+@pytest.mark.parametrize("k,p,S,threads", [(128, 32, 64 * 33, 1), (128, 32, 64 * 33, 4), (10, 4, 4096, 3),
+                                           (37, 9, 640, 2), (1024, 256, 128, 2), (3, 7, 64, 1), (200, 100, 192, 8)])
+def test_simd_port_matches_scalar_oracle(k, p, S, threads):
+    """The AVX2 port bench.py times as the CPU baseline computes the oracle's parity."""
+    if not orc.simd_available():
+        pytest.skip("no AVX2 on this CPU")
+    rng = np.random.default_rng(k + p + S + threads)
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    assert np.array_equal(orc.encode_simd(k, p, data, threads), orc.encode(16, k, p, data))
