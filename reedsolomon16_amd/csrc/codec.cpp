@@ -246,6 +246,12 @@ bool sub_enabled() {
     return !(e && e[0] == '1');
 }
 
+// RS_NO_PRUNE=1 disables the FFT group pruning of the LDS reconstruct (A/B experiments only).
+bool prune_enabled() {
+    const char *e = getenv("RS_NO_PRUNE");
+    return !(e && e[0] == '1');
+}
+
 // RS_NO_SPLIT=1 disables the split kernel (A/B experiments only).
 bool split_enabled() {
     const char *e = getenv("RS_NO_SPLIT");
@@ -614,6 +620,8 @@ int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipS
         ra.S = S;
         ra.mtrunc = c->m + c->k;
         ra.nd = nd;
+        ra.prune = prune_enabled() ? 1 : 0;
+        for (int p : pl.pos) ra.need[p >> 5] |= 1u << (p & 31);
         HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
         return RS_OK;
     }

@@ -1224,11 +1224,30 @@ struct LTile {
     __device__ static bool valid(uint64_t tile, uint64_t S, int u) { return tile + (uint64_t)(F::off(u) & ~63) < S; }
 };
 
+// Rows [lo, lo + cnt) (cnt a power of two, lo a multiple of cnt) hold a set
+// bit of the 256-bit row mask (wave-uniform words, lane-varying lo).
+__device__ __forceinline__ bool rows_needed(const uint32_t (&w)[8], int lo, int cnt) {
+    if (cnt >= 32) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k * 32 >= lo && k * 32 < lo + cnt) acc |= w[k];
+        return acc != 0;
+    }
+    uint32_t word = w[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++) word = (lo >> 5) == k ? w[k] : word;
+    return ((word >> (lo & 31)) & ((1u << cnt) - 1)) != 0;
+}
+
 // One radix-4 pass (rows i, i+d, i+2d, i+3d; twiddles m01, m02, m23 at
 // tw + 3*g) over the active groups, or a radix-2 pass, on the LDS rows.
+// need (forward passes only): skip groups none of whose rows is read later --
+// the pruning of errorBitfield.fftDIT (leopard16.go:1215-1252); the rows that
+// are read come out identical.
 template <class F, bool INV>
 __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int groups_active,
-                                         const uint32_t *__restrict__ tw) {
+                                         const uint32_t *__restrict__ tw, const uint32_t (*need)[8] = nullptr) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
     constexpr int U = L::U;
@@ -1239,6 +1258,7 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
             const int q = it / U, u = it - q * U;
             const int g = q >> ld, j = q & (dist - 1);
             const int i = g * 4 * dist + j;
+            if (!INV && need && !rows_needed(*need, g * 4 * dist, 4 * dist)) continue;
             const uint32_t *t = tw + (uint64_t)g * 3 * F::TWD;
             V x0 = L::get(lds, i, u), x1 = L::get(lds, i + dist, u), x2 = L::get(lds, i + 2 * dist, u),
               x3 = L::get(lds, i + 3 * dist, u);
@@ -1255,6 +1275,7 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
         for (int it = threadIdx.x; it < pairs * U; it += 256) {
             const int q = it / U, u = it - q * U;
             const int rx = INV ? q : 2 * q, ry = INV ? q + dist : 2 * q + 1;
+            if (!INV && need && !rows_needed(*need, 2 * q, 2)) continue;
             const uint32_t *t = INV ? tw : tw + (uint64_t)q * F::TWD;
             V x = L::get(lds, rx, u), y = L::get(lds, ry, u);
             if constexpr (INV) ifft2<F>(x, y, t);
@@ -1269,7 +1290,8 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
 // Full transform over 2^LOGN LDS rows with the reference's pass structure
 // (gf_host.cpp ifft_passes / fft_passes) and its mtrunc group skipping.
 template <class F, bool INV, int LOGN>
-__device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw) {
+__device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
+                                              const uint32_t (*need)[8] = nullptr) {
     constexpr int N = 1 << LOGN;
     int slot = 0;
     if constexpr (INV) {
@@ -1288,13 +1310,13 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
             const int groups = N / (4 * dist);
             int active = (mtrunc + 4 * dist - 1) / (4 * dist);
             if (active > groups) active = groups;
-            lds_pass<F, false>(lds, dist, 4, active, tw + (uint64_t)slot * F::TWD);
+            lds_pass<F, false>(lds, dist, 4, active, tw + (uint64_t)slot * F::TWD, need);
             slot += 3 * groups;
         }
         if (LOGN & 1) {
             int active = (mtrunc + 1) / 2;
             if (active > N / 2) active = N / 2;
-            lds_pass<F, false>(lds, 1, 2, active, tw + (uint64_t)slot * F::TWD);
+            lds_pass<F, false>(lds, 1, 2, active, tw + (uint64_t)slot * F::TWD, need);
         }
     }
 }
@@ -1344,7 +1366,14 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         }
         __syncthreads();
     }
-    lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft);
+    if (a.prune) {
+        uint32_t need[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) need[k] = __builtin_amdgcn_readfirstlane(a.need[k]);
+        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, &need);
+    } else {
+        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft);
+    }
     // reveal: shard = work[pos] * (modulus - errLocs[pos])
     for (int it = threadIdx.x; it < a.nd * U; it += 256) {
         const int j = it / U, u = it - j * U;

@@ -76,6 +76,10 @@ struct RecArgs {
     uint64_t S;
     int mtrunc;                 // m + k
     int nd;
+    // errorBitfield analog (leopard16.go:1076-1252): bit r set when work row r
+    // is revealed; FFT groups whose rows are all unset are skipped.
+    int prune;
+    uint32_t need[8];           // n <= 256 rows
 };
 // sub: GF(2^16) transforms in subfield coordinates (tw_ifft/tw_fft are
 // kTwDwords8 subfield tables; tw_in/tw_out fold in the coordinate change).

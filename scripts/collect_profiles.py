@@ -27,7 +27,7 @@ def path_of(name: str):
     """Kernel symbol -> the engine's path name (codec.cpp plan_encode_host)."""
     def v(flag):
         return "-verify" if flag == "true" else ""
-    m = re.search(r"k_encode_bs<.*BsTw<\d+, \d+>, (false|true)>", name)
+    m = re.search(r"k_encode_(?:bs|hp)<.*BsTw<\d+, \d+>, (false|true)>", name)
     if m:
         return "bs16-m32" + v(m.group(1))
     m = re.search(r"k_encode_split<(\d+), (false|true)>", name)
@@ -87,7 +87,7 @@ def main():
                       "round": tag}
         lines.append(f"{p}: FETCH_SIZE {fetch/1e6:.2f} MB (x2 = {2*fetch/1e6:.2f}), WRITE_SIZE {write/1e6:.2f} MB, "
                      f"HBM {hbm/1e6:.2f} MB/launch over {len(fk)} launches")
-    kern = [r for r in rows if "k_enc" in r["Name"]]
+    kern = [r for r in rows if "k_enc" in r["Name"] or "k_rec" in r["Name"]]
     for r in kern:
         lines.append(f"trace {short(r['Name'])}: calls {r['Calls']} avg {float(r['AverageNs'])/1e3:.2f} us "
                      f"min {float(r['MinNs'])/1e3:.2f} max {float(r['MaxNs'])/1e3:.2f}")

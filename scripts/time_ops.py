@@ -12,6 +12,11 @@ CONFIGS = {
     "C3": (16, 128, 32, 1 << 20, "encode"),
     "C3v": (16, 128, 32, 1 << 20, "verify"),
     "C4": (16, 128, 32, 1 << 20, "reconstruct"),
+    # few-erasure repair (the reference prunes its FFT below p/4 erasures): C4 geometry, e erased shards
+    "C4e1": (16, 128, 32, 1 << 20, "reconstruct", 1, 1),
+    "C4e2": (16, 128, 32, 1 << 20, "reconstruct", 1, 2),
+    "C4e4": (16, 128, 32, 1 << 20, "reconstruct", 1, 4),
+    "C4e8": (16, 128, 32, 1 << 20, "reconstruct", 1, 8),
     "C5": (16, 1024, 256, 256 << 10, "encode"),
     "C5x8": (16, 1024, 256, 32 << 10, "encode"),
     # encode batches: stripes per launch (rs_encode_dev_batch), so a small
@@ -82,11 +87,12 @@ def main():
             continue
         bits, k, p, S, op = CONFIGS[name][:5]
         ns = CONFIGS[name][5] if len(CONFIGS[name]) > 5 else 1
+        ne = CONFIGS[name][6] if len(CONFIGS[name]) > 6 else p
         c = rs.ReedSolomon(k, p, bits)
         slab = torch.randint(0, 256, (ns, k + p, S), dtype=torch.uint8, device="cuda")
         rows = slab[0]
         present = np.ones(k + p, bool)
-        present[np.random.default_rng(0x5EED).choice(k + p, p, replace=False)] = False
+        present[np.random.default_rng(0x5EED).choice(k + p, ne, replace=False)] = False
 
         def run():
             if op == "encode":
@@ -107,7 +113,8 @@ def main():
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.iters
         alg = ns * (k + p) * S
-        print(json.dumps({"tag": a.tag, "config": name, "op": op, "path": c.encode_path, "us": round(us, 2),
+        print(json.dumps({"tag": a.tag, "config": name, "op": op, "path": c.encode_path, "erased": int(ne) if op == "reconstruct" else 0,
+                          "prune": os.environ.get("RS_NO_PRUNE", "0") != "1", "us": round(us, 2),
                           "GBps_alg": round(alg / us / 1e3, 1), "frac": round(alg / us / 1e3 / 8000, 4)}), flush=True)
 
 

@@ -148,3 +148,31 @@ def test_gf8_inversion_cache_sequence():
     sh = [None if i == 0 else full[i].copy() for i in range(k + p)]
     c.reconstruct_data(sh)
     assert np.array_equal(sh[0], full[0])  # the engine's (correct) result
+
+
+@pytest.mark.parametrize("bits,k,p", [(16, 128, 32), (8, 128, 32), (16, 100, 28), (8, 10, 4)])
+@pytest.mark.parametrize("nerased", [1, 2, 3, 8])
+def test_pruned_fft_equals_unpruned_and_oracle(torch, monkeypatch, bits, k, p, nerased):
+    """The LDS reconstruct skips FFT groups whose rows are not revealed (the
+    analog of errorBitfield, leopard16.go:1076-1252 / leopard8.go:1165-1273):
+    the rebuilt rows equal the unpruned run (RS_NO_PRUNE=1) and the oracle."""
+    S = 4096 + 256
+    rng = np.random.default_rng(k + p + nerased + bits)
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    par = orc.encode(bits, k, p, data)
+    full = np.concatenate([data, par])
+    nerased = min(nerased, p)
+    for trial in range(3):
+        er = rng.choice(k + p, nerased, replace=False)
+        mask = np.zeros(k + p, bool)
+        mask[er] = True
+        outs = []
+        for noprune in ("0", "1"):
+            monkeypatch.setenv("RS_NO_PRUNE", noprune)
+            c = rs.ReedSolomon(k, p, bits)
+            slab = torch.from_numpy(full.copy()).cuda()
+            slab[torch.from_numpy(np.flatnonzero(mask)).cuda()] = 0
+            c.reconstruct_dev(slab, ~mask)
+            torch.cuda.synchronize()
+            outs.append(slab.cpu().numpy())
+        assert np.array_equal(outs[0], full) and np.array_equal(outs[1], full), (trial, sorted(er))
