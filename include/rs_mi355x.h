@@ -69,6 +69,20 @@ int rs_shard_size_multiple(const rs_codec *codec); /* 64: leopard16.go:58-60 */
  * leopard8.go:141-150.  Writes parity into shards[k..k+p). */
 int rs_encode(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards);
 
+/* Asynchronous Encode for stream pipelining (the analog of rsStream16.encode's
+ * per-block loop, streaming16.go:1229-1318): queues the stripe's copy-in,
+ * kernels and copy-out behind the codec's previous calls and returns; block
+ * j+1's host-to-device copies overlap block j's kernels and device-to-host
+ * copies.  The shards must stay valid (and the data rows unmodified) until the
+ * ticket completes.  Parity rows in pageable memory make the call synchronous
+ * (they go through the pinned bounce slab); pin them (rs_host_alloc /
+ * rs_host_register) for overlap.  Same validation and errors as rs_encode. */
+int rs_encode_async(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards, uint64_t *ticket);
+/* Block until the encode behind `ticket` has written its parity rows. */
+int rs_encode_wait(rs_codec *codec, uint64_t ticket);
+/* *done = 1 when it has, 0 otherwise (no blocking). */
+int rs_encode_query(rs_codec *codec, uint64_t ticket, int *done);
+
 /* Verify: leopard16.go:361-387 / leopard8.go:415-436.  *ok = 1 iff parity matches. */
 int rs_verify(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards, int *ok);
 

@@ -30,6 +30,9 @@ def lib() -> C.CDLL:
     for fn in ("rs_field_bits", "rs_data_shards", "rs_parity_shards", "rs_total_shards", "rs_shard_size_multiple"):
         getattr(L, fn).argtypes = [vp]
     L.rs_encode.argtypes = [vp, P(vp), P(sz), i32]
+    L.rs_encode_async.argtypes = [vp, P(vp), P(sz), i32, P(C.c_uint64)]
+    L.rs_encode_wait.argtypes = [vp, C.c_uint64]
+    L.rs_encode_query.argtypes = [vp, C.c_uint64, P(i32)]
     L.rs_verify.argtypes = [vp, P(vp), P(sz), i32, P(i32)]
     L.rs_reconstruct.argtypes = [vp, P(vp), P(sz), i32, i32]
     L.rs_encode_idx.argtypes = [vp, vp, sz, i32, P(vp), P(sz), i32]

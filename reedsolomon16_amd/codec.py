@@ -227,6 +227,16 @@ class ReedSolomon:
         ptrs, lens, _keep = _host_rows(shards)
         _check(self._L.rs_encode(self._h, ptrs, lens, len(shards)))
 
+    def encode_async(self, shards: list) -> "EncodeTicket":
+        """Queue an Encode behind the codec's previous calls (rs_encode_async):
+        the copies and kernels of consecutive stripes overlap.  Keep `shards`
+        alive and unmodified until the ticket's wait() returns; pinned parity
+        rows (alloc_aligned(pinned=True)) are needed for the call to return early."""
+        ptrs, lens, keep = _host_rows(shards)
+        t = C.c_uint64(0)
+        _check(self._L.rs_encode_async(self._h, ptrs, lens, len(shards), C.byref(t)))
+        return EncodeTicket(self, t.value, keep)
+
     def verify(self, shards: list) -> bool:
         """Verify (leopard16.go:361-387)."""
         ptrs, lens, _keep = _host_rows(shards)
@@ -396,6 +406,22 @@ class ReedSolomon:
         n, _, S = slab.shape
         _check(self._L.rs_encode_dev_batch(self._h, slab.data_ptr(), slab.stride(1), slab.stride(0), n, S,
                                            _stream_handle(stream)))
+
+
+class EncodeTicket:
+    """Completion handle of ReedSolomon.encode_async (holds the shard arrays alive)."""
+
+    def __init__(self, codec: ReedSolomon, ticket: int, keep):
+        self.codec, self.ticket, self._keep = codec, ticket, keep
+
+    def done(self) -> bool:
+        d = C.c_int(0)
+        _check(self.codec._L.rs_encode_query(self.codec._h, self.ticket, C.byref(d)))
+        return bool(d.value)
+
+    def wait(self) -> None:
+        _check(self.codec._L.rs_encode_wait(self.codec._h, self.ticket))
+        self._keep = None
 
 
 def New(data_shards: int, parity_shards: int, device: Optional[int] = None) -> ReedSolomon:

@@ -142,6 +142,13 @@ struct rs_codec {
     hipEvent_t ev_in[kHostBufs] = {}, ev_k[kHostBufs] = {}, ev_free[kHostBufs] = {};
     DevBuf<uint8_t> stage;
     uint64_t host_seg_bytes = 0;  // 0: automatic
+    // staging-slab rotation continues across calls, so the segments of an
+    // asynchronous encode queue behind the previous call's (rs_encode_async)
+    uint64_t pipe_seq = 0;
+    // asynchronous encodes: ticket t completes at done_ev[t % kTickets]
+    static constexpr int kTickets = 64;
+    hipEvent_t done_ev[kTickets] = {};
+    uint64_t next_ticket = 1;
     // pinned bounce slabs for outputs in pageable host memory (kHostBufs x total x seg)
     uint8_t *bounce = nullptr;
     size_t bounce_n = 0;
@@ -164,6 +171,8 @@ struct rs_codec {
         if (s_out) (void)hipStreamSynchronize(s_out);
         stage.release();
         if (bounce) (void)hipHostFree(bounce);
+        for (int t = 0; t < kTickets; t++)
+            if (done_ev[t]) (void)hipEventDestroy(done_ev[t]);
         for (int b = 0; b < kHostBufs; b++) {
             if (ev_in[b]) (void)hipEventDestroy(ev_in[b]);
             if (ev_k[b]) (void)hipEventDestroy(ev_k[b]);
@@ -774,11 +783,24 @@ size_t split_per_shard(const rs_codec *c, size_t len) {
     return (per + 63) / 64 * 64;
 }
 
+// Drains nothing on success when the call is asynchronous.
+struct PipeDrainIf {
+    rs_codec *c;
+    bool armed = true;
+    ~PipeDrainIf() {
+        if (!armed) return;
+        PipeDrain d{c};
+    }
+};
+
+// ticket != nullptr: asynchronous encode (outputs in pinned or device memory):
+// returns after queueing every segment; *ticket completes when the parity is
+// in the caller's rows (rs_encode_wait).
 int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, const std::vector<uint8_t> &present,
-                  bool recover_all, int *ok) {
+                  bool recover_all, int *ok, uint64_t *ticket = nullptr) {
     int e = ensure_host_pipe(c);
     if (e) return e;
-    PipeDrain drain_guard{c};
+    PipeDrainIf drain_guard{c};
     hipStream_t sc = c->stream;
     e = scratch_acquire(c, sc);
     if (e) return e;
@@ -798,7 +820,14 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     }
     const uint64_t seg = host_segment(c, S, in_rows.size());
     const uint64_t slab = (uint64_t)total * seg;
-    HIP_TRY(c->stage.ensure((size_t)kHostBufs * slab));
+    if (c->stage.n < (size_t)kHostBufs * slab) {  // a reallocation waits for queued segments
+        HIP_TRY(hipStreamSynchronize(c->s_in));
+        HIP_TRY(hipStreamSynchronize(sc));
+        HIP_TRY(hipStreamSynchronize(c->s_out));
+        HIP_TRY(c->stage.ensure((size_t)kHostBufs * slab));
+        c->pipe_seq = 0;
+    }
+    // slabs keep their (kHostBufs) rotation across calls: each call starts at pipe_seq
     // scratch of the multi-pass paths, sized before any launch (no realloc mid-pipeline)
     if (op == HostOp::Reconstruct) e = scratch_ensure(c, c->work, (size_t)c->n * seg);
     else if (c->logm > kMaxRegLogM) e = scratch_ensure(c, c->work, (size_t)2 * c->m * seg);
@@ -807,6 +836,7 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     // copies segment j - 1 out while the device works on segment j
     bool use_bounce = false;
     for (int r : out_rows) use_bounce = use_bounce || is_pageable(shards[r]);
+    const bool async = ticket && !use_bounce;  // pageable outputs need the host drain: synchronous
     std::vector<std::vector<uint8_t *>> btab(kHostBufs, std::vector<uint8_t *>(total));
     if (use_bounce) {
         const size_t need = (size_t)kHostBufs * slab;
@@ -820,8 +850,9 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
         for (int b = 0; b < kHostBufs; b++)
             for (int i = 0; i < total; i++) btab[b][i] = c->bounce + b * slab + (uint64_t)i * seg;
     }
+    const uint64_t seq0 = c->pipe_seq;
     auto drain = [&](uint64_t j) -> int {  // host copy of segment j's outputs out of its bounce slab
-        const int b = (int)(j % kHostBufs);
+        const int b = (int)((seq0 + j) % kHostBufs);
         const uint64_t off = j * seg, w = std::min(seg, S - off);
         HIP_TRY(hipEventSynchronize(c->ev_free[b]));
         for (int r : out_rows) std::memcpy(shards[r] + off, btab[b][r], w);
@@ -829,6 +860,10 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     };
     std::vector<std::vector<uint8_t *>> sets(kHostBufs, std::vector<uint8_t *>(total));
     if (op == HostOp::Reconstruct) {
+        // the blob's per-set row tables point into the slabs; a reconstruct
+        // waits for every queued segment before it rewrites the blob
+        HIP_TRY(hipStreamSynchronize(c->s_out));
+        HIP_TRY(hipStreamSynchronize(sc));
         std::vector<uint8_t *const *> d;
         for (int b = 0; b < kHostBufs; b++) {
             for (int i = 0; i < total; i++) sets[b][i] = c->stage.p + b * slab + (uint64_t)i * seg;
@@ -839,14 +874,18 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     }
     if (op == HostOp::Verify) HIP_TRY(hipMemsetAsync(c->dflag, 0, sizeof(int), sc));
     // copies in must not start before this call's setup on the compute stream
-    HIP_TRY(hipEventRecord(c->ev_k[0], sc));
-    HIP_TRY(hipStreamWaitEvent(c->s_in, c->ev_k[0], 0));
+    // (reconstruct tables, verify flag); an encode has none, and waiting here
+    // would queue its copy-in behind every kernel of the previous call
+    if (op != HostOp::Encode) {
+        HIP_TRY(hipEventRecord(c->ev_k[0], sc));
+        HIP_TRY(hipStreamWaitEvent(c->s_in, c->ev_k[0], 0));
+    }
     const uint64_t nseg = (S + seg - 1) / seg;
     for (uint64_t j = 0; j < nseg; j++) {
-        const int b = (int)(j % kHostBufs);
+        const int b = (int)((seq0 + j) % kHostBufs);
         const uint64_t off = j * seg, w = std::min(seg, S - off);
         uint8_t *st = c->stage.p + b * slab;
-        if (j >= (uint64_t)kHostBufs) HIP_TRY(hipStreamWaitEvent(c->s_in, c->ev_free[b], 0));
+        if (seq0 + j >= (uint64_t)kHostBufs) HIP_TRY(hipStreamWaitEvent(c->s_in, c->ev_free[b], 0));
         e = copy_rows(st, seg, shards, in_rows, off, w, true, c->s_in);
         if (e) return e;
         HIP_TRY(hipEventRecord(c->ev_in[b], c->s_in));
@@ -873,12 +912,24 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
             HIP_TRY(hipEventRecord(c->ev_free[b], sc));
         }
     }
+    c->pipe_seq = seq0 + nseg;
     if (op == HostOp::Verify) HIP_TRY(hipMemcpyAsync(c->hflag, c->dflag, sizeof(int), hipMemcpyDeviceToHost, sc));
     e = scratch_release(c, sc);
     if (e) return e;
     if (use_bounce && nseg) {
         e = drain(nseg - 1);
         if (e) return e;
+    }
+    if (ticket) {
+        const uint64_t t = c->next_ticket++;
+        hipEvent_t &ev = c->done_ev[t % rs_codec::kTickets];
+        if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ev, out_rows.empty() ? sc : c->s_out));
+        *ticket = t;
+        if (async) {
+            drain_guard.armed = false;
+            return RS_OK;
+        }
     }
     HIP_TRY(hipStreamSynchronize(c->s_in));
     HIP_TRY(hipStreamSynchronize(sc));
@@ -1183,6 +1234,56 @@ int rs_encode(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshar
     DeviceGuard g(c->device);
     if (int ie = ensure_device(c)) return ie;
     return host_pipeline(c, shards, S, HostOp::Encode, {}, true, nullptr);
+}
+
+int rs_encode_async(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshards, uint64_t *ticket) {
+    if (!c || !shards || !lens || !ticket) return RS_ERR_INVALID_ARG;
+    if (nshards != c->total) return RS_ERR_TOO_FEW_SHARDS;
+    int e = check_shards(lens, nshards, false);
+    if (e) return e;
+    const uint64_t S = shard_size_of(lens, nshards);
+    if (S % 64) return RS_ERR_INVALID_SHARD_SIZE;
+    if (!c->enc_ok) return RS_ERR_PANIC;
+    for (int i = 0; i < nshards; i++)
+        if (!shards[i]) return RS_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (int ie = ensure_device(c)) return ie;
+    return host_pipeline(c, shards, S, HostOp::Encode, {}, true, nullptr, ticket);
+}
+
+int rs_encode_query(rs_codec *c, uint64_t ticket, int *done) {
+    if (!c || !done) return RS_ERR_INVALID_ARG;
+    hipEvent_t ev;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (ticket == 0 || ticket >= c->next_ticket) return RS_ERR_INVALID_ARG;
+        ev = c->done_ev[ticket % rs_codec::kTickets];
+    }
+    DeviceGuard g(c->device);
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipErrorNotReady) {
+        *done = 0;
+        return RS_OK;
+    }
+    HIP_TRY(q);
+    *done = 1;
+    return RS_OK;
+}
+
+int rs_encode_wait(rs_codec *c, uint64_t ticket) {
+    if (!c) return RS_ERR_INVALID_ARG;
+    hipEvent_t ev;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (ticket == 0 || ticket >= c->next_ticket) return RS_ERR_INVALID_ARG;
+        // an event slot reused by a later call completes after this ticket's
+        // work (same streams, queue order): waiting on it is still correct
+        ev = c->done_ev[ticket % rs_codec::kTickets];
+    }
+    DeviceGuard g(c->device);
+    HIP_TRY(hipEventSynchronize(ev));
+    return RS_OK;
 }
 
 int rs_verify(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshards, int *ok) {

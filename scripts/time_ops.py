@@ -31,6 +31,10 @@ HOST_CONFIGS = {
     "H3p": (16, 128, 32, 1 << 20, "encode", True),
     "H4p": (16, 128, 32, 1 << 20, "reconstruct", True),
     "H3vp": (16, 128, 32, 1 << 20, "verify", True),
+    # a stream of 8 stripes (pinned), encoded one call at a time (sync) or
+    # queued with rs_encode_async and waited at the end (async)
+    "H3s_sync": (16, 128, 32, 1 << 20, "stream_sync", True),
+    "H3s_async": (16, 128, 32, 1 << 20, "stream_async", True),
 }
 
 
@@ -43,6 +47,34 @@ def time_host(name, iters, tag):
 
     bits, k, p, S, op, pinned = HOST_CONFIGS[name]
     c = rs.ReedSolomon(k, p, bits)
+    if op.startswith("stream"):
+        nblk = 8
+        blocks = []
+        rng = np.random.default_rng(1)
+        for _ in range(nblk):
+            sh = c.alloc_aligned(S, pinned=True)
+            for i in range(k):
+                sh[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+            blocks.append(sh)
+
+        def run_stream():
+            if op == "stream_sync":
+                for sh in blocks:
+                    c.encode(sh)
+            else:
+                ts = [c.encode_async(sh) for sh in blocks]
+                for t in ts:
+                    t.wait()
+
+        run_stream()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            run_stream()
+        us = (time.perf_counter() - t0) / iters / nblk * 1e6
+        print(json.dumps({"tag": tag, "config": name, "op": op, "pinned": True, "us_per_stripe": round(us, 1),
+                          "data_GiBps": round(k * S / us * 1e6 / 2**30, 2),
+                          "pcie_GBps": round((k + p) * S / us / 1e3, 1)}), flush=True)
+        return
     shards = c.alloc_aligned(S, pinned=pinned)
     rng = np.random.default_rng(1)
     for i in range(k):

@@ -526,3 +526,31 @@ def test_split_into_device_slab_encode_join(torch_dev, k, p, n):
     dd = torch.from_numpy(data).cuda()
     slab2 = c.split_dev(dd)
     assert torch.equal(slab2[:k], slab[:k])
+
+
+def test_encode_async_stream_of_blocks():
+    """rs_encode_async over a stream of blocks (the rsStream16.encode loop,
+    streaming16.go:1229-1318): several stripes queued back to back through
+    the three-stream pipeline, pinned rows, then waited; each equals the
+    oracle.  Small segments force the slab rotation to continue across calls."""
+    k, p, S, nblk = 20, 8, 64 * 40, 6
+    c = rs.New16(k, p)
+    c.set_host_segment(64 * 7)
+    rng = np.random.default_rng(99)
+    blocks, tickets = [], []
+    for b in range(nblk):
+        sh = c.alloc_aligned(S, pinned=True)
+        for i in range(k):
+            sh[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+        blocks.append(sh)
+        tickets.append(c.encode_async(sh))
+    for t in tickets[::-1]:
+        t.wait()
+    assert all(t.done() for t in tickets)
+    for sh in blocks:
+        assert np.array_equal(np.stack(sh[k:]), orc.encode(16, k, p, np.stack(sh[:k])))
+    # pageable parity rows: the call completes synchronously, same result
+    sh = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+    t = c.encode_async(sh)
+    t.wait()
+    assert np.array_equal(np.stack(sh[k:]), orc.encode(16, k, p, np.stack(sh[:k])))
