@@ -1168,6 +1168,9 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 // tile must cover whole 64-byte blocks (low bytes [0,32), high bytes
 // [32,64)), so W = 1 (32-byte tiles) is invalid: the parity tests reject it.
 constexpr uint64_t kLdsMinGrid = 512;
+#ifndef RS_LDS_PAD
+#define RS_LDS_PAD 16  // LDS row padding of the LDS-resident kernels (bytes)
+#endif
 
 // RS_UNIT_WIDTH=wide / narrow forces the per-launch unit-width choices below
 // (LDS tiles of 128 vs 64 bytes; GF(2^8) register units of 16 vs 4 bytes) so
@@ -1187,7 +1190,7 @@ struct LTile {
     static_assert(!F::SYM16 || F::W >= 2, "a GF(2^16) LDS tile must cover whole 64-byte blocks (W >= 2)");
     static constexpr bool W16 = F::SYM16;
     static constexpr int TB = 32 * F::W;                  // bytes of each row owned by a workgroup
-    static constexpr int ROW = TB + 16;                   // LDS row stride (144 B at TB = 128 spreads rows over the banks)
+    static constexpr int ROW = TB + RS_LDS_PAD;           // LDS row stride (TB + 16 = 144 B at TB = 128)
     static constexpr int UB = W16 ? 8 * F::W : 4 * F::W;  // global bytes per unit
     static constexpr int U = TB / UB;                     // units per tile
     typedef typename F::Vec V;
