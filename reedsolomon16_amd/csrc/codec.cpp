@@ -98,7 +98,7 @@ struct rs_codec {
     std::vector<uint32_t> enc_ifft_logs, enc_fft_logs;
     DevBuf<uint32_t> tw_ifft, tw_fft;
     bool split_ok = false;            // half-wave split kernel available (GF(2^16), 4 <= m <= 32)
-    bool bs_ok = false;               // bit-sliced kernel compiled in for (k, p) (GF(2^16), m = 32)
+    bool bs_ok = false;               // bit-sliced kernel covers (k, p) (GF(2^16), m = 16 or 32)
     int cus = 0;                      // compute units of the device (persistent grids)
     DevBuf<uint32_t> tws_ifft, tws_fft;  // its twiddle images (schedule.hpp EncodeSplit)
     std::string path;
@@ -274,8 +274,9 @@ void plan_encode_host(rs_codec *c) {
                                                    : c->logm <= kMaxLdsLogN ? "lds-m" + std::to_string(c->m) : "multipass");
     if (c->enc_ok && c->bits == 16 && c->logm >= 2 && c->logm <= 5 && split_enabled())
         c->path = std::string("split16-m") + std::to_string(c->m);
-    c->bs_ok = c->enc_ok && c->bits == 16 && c->logm == 5 && bs_enabled() && encode_bs_available(c->k, c->p);
-    if (c->bs_ok) c->path = "bs16-m32";
+    c->bs_ok = c->enc_ok && c->bits == 16 && (c->logm == 4 || c->logm == 5) && bs_enabled() &&
+               encode_bs_available(c->k, c->p, c->enc_ifft_logs.data(), c->enc_fft_logs.data(), c->F->mod);
+    if (c->bs_ok) c->path = std::string("bs16-m") + std::to_string(c->m);
 }
 
 // Device half, on first use: stream, flag word, encode twiddle tables.
@@ -439,7 +440,9 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
         a.tw_fft = c->tw_fft.p;
         a.mismatch = mismatch;
         // bit-sliced kernel: strided rows, one row stride for data and parity
-        if (c->bs_ok && !data.table && !par.table && data.stride == par.stride && data.stride >= S) {
+        const uint64_t span = (uint64_t)(c->k - 1) * data.stride + S;
+        if (c->bs_ok && !data.table && !par.table && data.stride == par.stride && data.stride >= S &&
+            (uint64_t)(std::max(c->k, c->p) - 1) * data.stride + S < (1ull << 32)) {
             BsArgs b{};
             b.data = data.base;
             b.parity = par.base;
@@ -455,7 +458,6 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
             return RS_OK;
         }
         // split kernel: strided rows whose data span fits a 32-bit buffer offset
-        const uint64_t span = (uint64_t)(c->k - 1) * data.stride + S;
         if (c->split_ok && !data.table && !par.table && span < (1ull << 32)) {
             a.tw_ifft = c->tws_ifft.p;
             a.tw_fft = c->tws_fft.p;

@@ -88,19 +88,24 @@ hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStr
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 
 
-// ---- Bit-sliced encode (csrc/bitslice.hip): GF(2^16), m = 32, geometries
-// compiled in at build time (Makefile BS_CONFIGS).  Strided rows only.
+// ---- Bit-sliced encode (csrc/bitslice.hip): GF(2^16), m = 16 or 32
+// (9 <= p <= 32), k up to the chunk count compiled into the per-m tables
+// (Makefile BS_CHUNKS).  Strided rows, one row stride for data and parity.
 struct BsArgs {
     const uint8_t *data;    // stripe 0, data row 0
     uint8_t *parity;        // stripe 0, parity row 0
     uint64_t row_stride, stripe_stride, S;
     int k, p, nstripes;
-    int tiles_per_stripe, ntiles;  // set by the launcher (tile width depends on the kernel)
+    int tiles_per_stripe, ntiles;  // set by the launcher
     uint32_t span, pspan;          // set by the launcher: (k-1)*row_stride + S, (p-1)*row_stride + S
     int *mismatch;          // verify
 };
-bool encode_bs_available(int k, int p);
+// True when the tables cover (k, p) and agree with the geometry's own
+// schedule (encode_schedule: nchunks * ifft_slots(logm) IFFT logs, then
+// fft_slots(logm) FFT logs; entries == mod are truncated groups).
+bool encode_bs_available(int k, int p, const uint32_t *ifft_logs, const uint32_t *fft_logs, uint32_t mod);
 // cus: compute units of the device (the launcher sizes its persistent grid).
+// hipErrorNotSupported when the rows of one stripe span >= 4 GiB (32-bit buffer offsets).
 hipError_t launch_encode_bs(bool verify, const BsArgs &a, int cus, hipStream_t s);
 
 }  // namespace rs

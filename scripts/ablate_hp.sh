@@ -9,7 +9,7 @@ SRC=reedsolomon16_amd/csrc
 B=reedsolomon16_amd/build
 OUT=build/ablate_hp
 rm -rf $OUT; mkdir -p $OUT/common
-$B/gen_bs_tables $OUT/common/bs_tables.h ${BS_CONFIGS:-128:32}
+$B/gen_bs_tables $OUT/common/bs_tables.h ${BS_CHUNKS:-4:12 5:6}
 for v in ${VARIANTS:-base: nomul:-DRS_BS_ABL_NOMUL nolds:-DRS_BS_ABL_NOLDS noload:-DRS_BS_ABL_NOLOAD notrans:-DRS_BS_ABL_NOTRANS nostore:-DRS_BS_ABL_NOSTORE memonly:-DRS_BS_ABL_NOMUL,-DRS_BS_ABL_NOTRANS,-DRS_BS_ABL_NOLDS}; do
   name=${v%%:*}; flags=${v#*:}; flags=${flags//,/ }
   mkdir -p $OUT/$name

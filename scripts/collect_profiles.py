@@ -27,9 +27,9 @@ def path_of(name: str):
     """Kernel symbol -> the engine's path name (codec.cpp plan_encode_host)."""
     def v(flag):
         return "-verify" if flag == "true" else ""
-    m = re.search(r"k_encode_(?:bs|hp)<.*BsTw<\d+, \d+>, (false|true)>", name)
+    m = re.search(r"k_encode_hp<(\d+), (false|true)>", name)
     if m:
-        return "bs16-m32" + v(m.group(1))
+        return f"bs16-m{1 << int(m.group(1))}" + v(m.group(2))
     m = re.search(r"k_encode_split<(\d+), (false|true)>", name)
     if m:
         return f"split16-m{1 << int(m.group(1))}" + v(m.group(2))

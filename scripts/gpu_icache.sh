@@ -11,7 +11,7 @@ f = glob.glob("gpurun_out/icache/**/*counter_collection.csv", recursive=True)[0]
 acc = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
 for r in csv.DictReader(open(f)):
     k = r["Kernel_Name"]
-    if "k_encode_bs" not in k: continue
+    if "k_encode_hp" not in k: continue
     acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
     n[(k, r["Counter_Name"])] += 1
 for k, d in acc.items():

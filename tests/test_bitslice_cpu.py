@@ -4,13 +4,16 @@ built from, no device calls:
 * its 64-byte block <-> bit-plane transpose (three delta-swap stages per
   8-dword half, restated in numpy) puts bit b of symbol 4w+j at bit 8j+w of
   plane b, and is an involution;
-* the twiddle matrices tools/gen_bs_tables.cpp writes into build/bs_tables.h,
-  applied as GF(2) matrices in the kernel's pass and butterfly order (chunk
-  IFFT passes 1-3, XOR-accumulate, FFT passes A-C), give the oracle's parity
-  bit for bit (leopard16.go:128-224) for every geometry compiled in;
-* the same for the half-plane kernel's order (k_encode_hp: IFFT layers
-  r0-r2 per 8-row group, layers r3-r4 per coset, FFT layers r4-r3 per coset,
-  r2-r0 per group) and its slot indexing.
+* the per-m twiddle tables tools/gen_bs_tables.cpp writes into
+  build/bs_tables.h (HpTab<LOGM>: 8x8 matrices in subfield coordinates, one
+  table per m for every k and p), applied in the half-plane kernel's order
+  (k_encode_hp: IFFT layers r0..r(LR-1) per row group, r(LR), r(LR+1) per
+  coset, XOR-accumulate, FFT layers r(LR+1), r(LR) per coset, then
+  r(LR-1)..r0 per row group) with its slot indexing (bitslice.hip
+  ifft_slot / fft_slot, restated here), give the oracle's parity bit for bit
+  (leopard16.go:128-224) for m = 16 and 32 and ragged k and p;
+* the logs behind the matrices equal the geometry's own schedule wherever
+  the reference does not truncate (the host check the codec runs).
 """
 import os
 import re
@@ -62,28 +65,32 @@ def load_tables():
         pytest.skip("build/bs_tables.h not generated (run __graft_entry__.build())")
     txt = open(HDR).read()
     out = {}
-    for m in re.finditer(r"struct BsTw<(\d+), (\d+)> \{(.*?)\n\};", txt, re.S):
-        k, p, body = int(m.group(1)), int(m.group(2)), m.group(3)
-        nch = int(re.search(r"NCH = (\d+)", body).group(1))
-        v = np.array([int(x, 16) for x in re.findall(r"0x([0-9a-fA-F]{4})", body)], np.uint32)
-        assert v.size == (nch + 1) * 31 * 16, (k, p)
-        sub = None
-        if "SUB = true" in body:
-            def nums(name):
-                blk = re.search(r"\b" + name + r"\[[^=]*= *(\{.*?\});", body, re.S).group(1)
-                return np.array([int(x) for x in re.findall(r"\d+", blk)], np.uint32)
-            i8, f8 = nums("ifft8"), nums("fft8")
-            assert i8.size == nch * 31 * 8 and f8.size == 31 * 8
-            sub = (nums("dmat"), i8.reshape(nch, 31, 8), f8.reshape(31, 8))
-        out[(k, p)] = (v[:nch * 496].reshape(nch, 31, 16), v[nch * 496:].reshape(31, 16), sub)
-    assert out, "no geometry in bs_tables.h"
+    for m in re.finditer(r"struct HpTab<(\d+)> \{(.*?)\n\};", txt, re.S):
+        logm, body = int(m.group(1)), m.group(2)
+
+        def num(name):
+            return int(re.search(r"\b" + name + r" = (\d+)", body).group(1))
+
+        def arr(name):
+            blk = re.search(r"\b" + name + r"\[[^=]*= *(\{.*?\});", body, re.S).group(1)
+            return np.array([int(x) for x in re.findall(r"\d+", blk)], np.uint64)
+
+        nch, IS, FS = num("NCH"), num("IS"), num("FS")
+        out[logm] = dict(nch=nch, dmat=arr("dmat").astype(np.uint32),
+                         ifft8=arr("ifft8").astype(np.uint32).reshape(nch, IS, 8),
+                         fft8=arr("fft8").astype(np.uint32).reshape(FS, 8),
+                         ifft_log=arr("ifft_log").reshape(nch, IS), fft_log=arr("fft_log").reshape(FS))
+    assert out, "no table in bs_tables.h"
     return out
 
 
-def test_header_holds_makefile_geometries():
+def test_header_holds_makefile_tables():
     mk = open(os.path.join(ROOT, "reedsolomon16_amd", "Makefile")).read()
-    cfg = re.search(r"BS_CONFIGS \?= (.*)", mk).group(1).split()
-    assert {tuple(int(x) for x in c.split(":")) for c in cfg} == set(load_tables())
+    req = dict(tuple(int(x) for x in c.split(":")) for c in re.search(r"BS_CHUNKS \?= (.*)", mk).group(1).split())
+    tabs = load_tables()
+    assert set(tabs) == set(req) == {4, 5}
+    for logm, cap in req.items():
+        assert tabs[logm]["nch"] == cap, "every requested chunk lies in the subfield"
 
 
 def gf2_apply(rows, y):
@@ -92,66 +99,6 @@ def gf2_apply(rows, y):
     for i in range(16):
         out |= (np.bitwise_count(y & rows[i]) & 1).astype(np.uint32) << np.uint32(i)
     return out
-
-
-def bs_encode(tabs, k, p, sym):
-    """The kernel's schedule on symbols (rows of uint32 symbol values)."""
-    ifft, fft = tabs[0], tabs[1]
-
-    def i2(X, a, b, M):
-        X[b] ^= X[a]
-        X[a] ^= gf2_apply(M, X[b])
-
-    def f2(X, a, b, M):
-        X[a] ^= gf2_apply(M, X[b])
-        X[b] ^= X[a]
-
-    def i4(X, r, T, s):
-        i2(X, r[0], r[1], T[s])
-        i2(X, r[2], r[3], T[s + 2])
-        i2(X, r[0], r[2], T[s + 1])
-        i2(X, r[1], r[3], T[s + 1])
-
-    def f4(X, r, T, s):
-        f2(X, r[0], r[2], T[s + 1])
-        f2(X, r[1], r[3], T[s + 1])
-        f2(X, r[0], r[1], T[s])
-        f2(X, r[2], r[3], T[s + 2])
-
-    acc = None
-    for c in range(ifft.shape[0]):
-        X = np.zeros((32, sym.shape[1]), np.uint32)
-        n = min(32, k - 32 * c)
-        X[:n] = sym[32 * c:32 * c + n]
-        T = ifft[c]
-        for w in range(8):  # pass 1
-            i4(X, [4 * w + i for i in range(4)], T, 3 * w)
-        for h in range(2):  # pass 2
-            for j in range(4):
-                i4(X, [16 * h + j + 4 * i for i in range(4)], T, 24 + 3 * h)
-        for w in range(16):  # pass 3
-            i2(X, w, w + 16, T[30])
-        acc = X if acc is None else acc ^ X
-    for j in range(8):  # pass A
-        f4(acc, [j + 8 * i for i in range(4)], fft, 0)
-    for g in range(4):  # pass B
-        for j in range(2):
-            f4(acc, [8 * g + j + 2 * i for i in range(4)], fft, 3 + 3 * g)
-    for q in range(16):  # pass C
-        f2(acc, 2 * q, 2 * q + 1, fft[15 + q])
-    return acc[:p]
-
-
-@pytest.mark.parametrize("S", [64, 192])
-def test_tables_and_schedule_match_oracle(S):
-    for (k, p), tabs in load_tables().items():
-        rng = np.random.default_rng(k * 7 + p + S)
-        data = rng.integers(0, 256, (k, S), dtype=np.uint8)
-        blk = data.reshape(k, -1, 64)
-        sym = (blk[:, :, :32].astype(np.uint32) | (blk[:, :, 32:].astype(np.uint32) << 8)).reshape(k, -1)
-        par = bs_encode(tabs, k, p, sym).reshape(p, -1, 32)
-        got = np.concatenate([(par & 0xFF).astype(np.uint8), (par >> 8).astype(np.uint8)], axis=2).reshape(p, S)
-        assert np.array_equal(got, orc.encode(16, k, p, data)), (k, p)
 
 
 def to_sub(dmat, sym):
@@ -163,102 +110,126 @@ def to_sub(dmat, sym):
     return out
 
 
-def test_subfield_tables_match_oracle():
-    """SUB geometries: the same schedule with one 8x8 matrix on each byte half, in
-    subfield coordinates, reproduces the oracle."""
-    n = 0
-    for (k, p), (_, _, sub) in load_tables().items():
-        if sub is None:
-            continue
-        n += 1
-        dmat, i8, f8 = sub
-        # 8x8 rows -> the block-diagonal 16x16 rows the full-matrix emulation takes
-        def widen(t):
-            return (t | (t << np.uint32(8)))[..., list(range(8)) * 2] & np.concatenate(
-                [np.full(8, 0xFF, np.uint32), np.full(8, 0xFF00, np.uint32)])
-        tabs = (widen(i8), widen(f8))
-        rng = np.random.default_rng(k + p)
-        S = 128
-        data = rng.integers(0, 256, (k, S), dtype=np.uint8)
-        blk = data.reshape(k, -1, 64)
-        sym = (blk[:, :, :32].astype(np.uint32) | (blk[:, :, 32:].astype(np.uint32) << 8)).reshape(k, -1)
-        par = to_sub(dmat, bs_encode(tabs, k, p, to_sub(dmat, sym))).reshape(p, -1, 32)
-        got = np.concatenate([(par & 0xFF).astype(np.uint8), (par >> 8).astype(np.uint8)], axis=2).reshape(p, S)
-        assert np.array_equal(got, orc.encode(16, k, p, data)), (k, p)
-    assert n >= 1
+def widen(t):
+    """8x8 rows -> the block-diagonal 16x16 rows (one map per byte half)."""
+    return (t | (t << np.uint32(8)))[..., list(range(8)) * 2] & np.concatenate(
+        [np.full(8, 0xFF, np.uint32), np.full(8, 0xFF00, np.uint32)])
 
 
-def hp_encode(tabs, k, p, sym):
+def ifft_slot(logm, layer, row):
+    """bitslice.hip ifft_slot (gf_host.cpp ifft_passes slot order)."""
+    off, dist = 0, 1
+    while dist * 4 <= (1 << logm):
+        l0 = dist.bit_length() - 1
+        g = row // (4 * dist)
+        if layer == l0 + 1:
+            return off + 3 * g + 1
+        if layer == l0:
+            return off + 3 * g + (2 if (row // dist) & 2 else 0)
+        off += 3 * ((1 << logm) // (4 * dist))
+        dist *= 4
+    return off
+
+
+def fft_slot(logm, layer, row):
+    """bitslice.hip fft_slot (gf_host.cpp fft_passes slot order)."""
+    M = 1 << logm
+    off, dist4, dist = 0, M, M >> 2
+    while dist:
+        l0 = dist.bit_length() - 1
+        g = row // dist4
+        if layer == l0 + 1:
+            return off + 3 * g + 1
+        if layer == l0:
+            return off + 3 * g + (2 if (row // dist) & 2 else 0)
+        off += 3 * (M // dist4)
+        dist4, dist = dist, dist >> 2
+    return off + row // 2
+
+
+def pairs(layer, rows):
+    """Lower rows j of the pairs (j, j + 2^layer) among rows [0, rows)."""
+    return [j for j in range(rows) if not (j >> layer) & 1]
+
+
+def hp_encode(tab, logm, k, p, sym):
     """k_encode_hp's butterfly order and twiddle slots (bitslice.hip HpEncoder)."""
-    ifft, fft = tabs[0], tabs[1]
+    M, RW, LR = 1 << logm, 1 << (logm - 2), logm - 2
+    ifft, fft = widen(tab["ifft8"]), widen(tab["fft8"])
 
-    def i2(X, a, b, M):
+    def i2(X, a, b, Mx):
         X[b] ^= X[a]
-        X[a] ^= gf2_apply(M, X[b])
+        X[a] ^= gf2_apply(Mx, X[b])
 
-    def f2(X, a, b, M):
-        X[a] ^= gf2_apply(M, X[b])
+    def f2(X, a, b, Mx):
+        X[a] ^= gf2_apply(Mx, X[b])
         X[b] ^= X[a]
 
+    nch = -(-k // M)
+    assert nch <= tab["nch"]
     acc = None
-    for c in range(ifft.shape[0]):
-        X = np.zeros((32, sym.shape[1]), np.uint32)
-        n = min(32, k - 32 * c)
-        X[:n] = sym[32 * c:32 * c + n]
+    for c in range(nch):
+        X = np.zeros((M, sym.shape[1]), np.uint32)
+        n = min(M, k - M * c)
+        X[:n] = sym[M * c:M * c + n]
         T = ifft[c]
-        for w in range(4):  # phase 1: rows 8w + j, layers r0, r1, r2
-            b = 8 * w
-            for j in (0, 2, 4, 6):
-                i2(X, b + j, b + j + 1, T[3 * (2 * w + (j >> 2)) + (2 if j & 2 else 0)])
-            for j in (0, 1, 4, 5):
-                i2(X, b + j, b + j + 2, T[3 * (2 * w + (j >> 2)) + 1])
-            for j in range(4):
-                i2(X, b + j, b + j + 4, T[24 + 3 * (w >> 1) + (2 if w & 1 else 0)])
-        for co in range(8):  # phase 2: rows co + 8t, layers r3, r4
-            r = [co + 8 * t for t in range(4)]
-            i2(X, r[0], r[1], T[25])
-            i2(X, r[2], r[3], T[28])
-            i2(X, r[0], r[2], T[30])
-            i2(X, r[1], r[3], T[30])
+        for w in range(4):  # row groups RW*w + j: layers r0 .. r(LR-1)
+            for l in range(LR):
+                for j in pairs(l, RW):
+                    r = RW * w + j
+                    i2(X, r, r + (1 << l), T[ifft_slot(logm, l, r)])
+        for co in range(RW):  # cosets: rows co + RW*t, layers r(LR), r(LR+1)
+            r = [co + RW * t for t in range(4)]
+            i2(X, r[0], r[1], T[ifft_slot(logm, LR, 0)])
+            i2(X, r[2], r[3], T[ifft_slot(logm, LR, 2 * RW)])
+            i2(X, r[0], r[2], T[ifft_slot(logm, LR + 1, 0)])
+            i2(X, r[1], r[3], T[ifft_slot(logm, LR + 1, RW)])
         acc = X if acc is None else acc ^ X
-    for co in range(8):  # FFT layers r4, r3 per coset
-        r = [co + 8 * t for t in range(4)]
-        f2(acc, r[0], r[2], fft[1])
-        f2(acc, r[1], r[3], fft[1])
-        f2(acc, r[0], r[1], fft[0])
-        f2(acc, r[2], r[3], fft[2])
-    for w in range(4):  # FFT layers r2, r1, r0 per group
-        b, s0 = 8 * w, 3 + 3 * w
-        for j in range(4):
-            f2(acc, b + j, b + j + 4, fft[s0 + 1])
-        f2(acc, b, b + 2, fft[s0])
-        f2(acc, b + 1, b + 3, fft[s0])
-        f2(acc, b + 4, b + 6, fft[s0 + 2])
-        f2(acc, b + 5, b + 7, fft[s0 + 2])
-        for j in (0, 2, 4, 6):
-            f2(acc, b + j, b + j + 1, fft[15 + 4 * w + (j >> 1)])
+    for co in range(RW):
+        r = [co + RW * t for t in range(4)]
+        f2(acc, r[0], r[2], fft[fft_slot(logm, LR + 1, 0)])
+        f2(acc, r[1], r[3], fft[fft_slot(logm, LR + 1, RW)])
+        f2(acc, r[0], r[1], fft[fft_slot(logm, LR, 0)])
+        f2(acc, r[2], r[3], fft[fft_slot(logm, LR, 2 * RW)])
+    for w in range(4):
+        for l in reversed(range(LR)):
+            for j in pairs(l, RW):
+                r = RW * w + j
+                f2(acc, r, r + (1 << l), fft[fft_slot(logm, l, r)])
     return acc[:p]
 
 
-def test_half_plane_schedule_matches_oracle():
-    """k_encode_hp's order in subfield coordinates (the only mode it runs in)."""
-    n = 0
-    for (k, p), (_, _, sub) in load_tables().items():
-        if sub is None:
-            continue
-        n += 1
-        dmat, i8, f8 = sub
+GEOMS = [(128, 32), (32, 32), (100, 17), (130, 32), (192, 32), (1, 17), (64, 16), (9, 9), (192, 16), (33, 12),
+         (1, 9), (177, 16)]
 
-        def widen(t):
-            return (t | (t << np.uint32(8)))[..., list(range(8)) * 2] & np.concatenate(
-                [np.full(8, 0xFF, np.uint32), np.full(8, 0xFF00, np.uint32)])
-        tabs = (widen(i8), widen(f8))
-        rng = np.random.default_rng(3 * k + p)
-        S = 128
-        data = rng.integers(0, 256, (k, S), dtype=np.uint8)
-        blk = data.reshape(k, -1, 64)
-        sym = (blk[:, :, :32].astype(np.uint32) | (blk[:, :, 32:].astype(np.uint32) << 8)).reshape(k, -1)
-        par = to_sub(dmat, hp_encode(tabs, k, p, to_sub(dmat, sym))).reshape(p, -1, 32)
-        got = np.concatenate([(par & 0xFF).astype(np.uint8), (par >> 8).astype(np.uint8)], axis=2).reshape(p, S)
-        assert np.array_equal(got, orc.encode(16, k, p, data)), (k, p)
-    assert n >= 1
+
+@pytest.mark.parametrize("k,p", GEOMS)
+def test_half_plane_schedule_matches_oracle(k, p):
+    """k_encode_hp's order in subfield coordinates (the only mode it runs in)."""
+    tabs = load_tables()
+    logm = 5 if p > 16 else 4
+    tab = tabs[logm]
+    rng = np.random.default_rng(3 * k + p)
+    S = 128
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    blk = data.reshape(k, -1, 64)
+    sym = (blk[:, :, :32].astype(np.uint32) | (blk[:, :, 32:].astype(np.uint32) << 8)).reshape(k, -1)
+    par = to_sub(tab["dmat"], hp_encode(tab, logm, k, p, to_sub(tab["dmat"], sym))).reshape(p, -1, 32)
+    got = np.concatenate([(par & 0xFF).astype(np.uint8), (par >> 8).astype(np.uint8)], axis=2).reshape(p, S)
+    assert np.array_equal(got, orc.encode(16, k, p, data)), (k, p)
+
+
+def test_slot_functions_cover_every_slot():
+    """Every IFFT/FFT slot of the schedule is used by exactly the butterflies
+    gf_host.cpp assigns it: the kernel's (layer, row) -> slot maps hit every
+    slot, and each slot sees one layer."""
+    for logm in (4, 5):
+        M = 1 << logm
+        ifs, ffs = {}, {}
+        for l in range(logm):
+            for j in pairs(l, M):
+                ifs.setdefault(ifft_slot(logm, l, j), set()).add(l)
+                ffs.setdefault(fft_slot(logm, l, j), set()).add(l)
+        n_if = {4: 15, 5: 31}[logm]
+        assert sorted(ifs) == list(range(n_if)) and sorted(ffs) == list(range(n_if))
+        assert all(len(v) == 1 for v in list(ifs.values()) + list(ffs.values()))

@@ -128,8 +128,15 @@ def test_constructor_errors():
     c = rs.New(10, 4)
     assert c.field_bits == 8 and c.total_shards() == 14 and c.shard_size_multiple() == 64
     assert rs.New(200, 100).field_bits == 16
-    assert rs.New16(128, 32).encode_path == "bs16-m32"  # bit-sliced kernel compiled in for 128+32
-    assert rs.New16(130, 32).encode_path == "split16-m32"
+    # bit-sliced kernel: one table per m covers every k <= chunks * m, 9 <= p <= 32
+    assert rs.New16(128, 32).encode_path == "bs16-m32"
+    assert rs.New16(130, 32).encode_path == "bs16-m32"
+    assert rs.New16(192, 17).encode_path == "bs16-m32"
+    assert rs.New16(64, 16).encode_path == "bs16-m16"
+    assert rs.New16(192, 9).encode_path == "bs16-m16"
+    assert rs.New16(193, 32).encode_path == "split16-m32"  # 7 chunks: past the m = 32 table
+    assert rs.New16(193, 16).encode_path == "split16-m16"  # 13 chunks: past the m = 16 table
+    assert rs.New16(64, 8).encode_path == "split16-m8"
     assert rs.New16(10, 1).encode_path == "reg16-m1"
     assert rs.New16(1024, 256).encode_path == "lds-m256"
     assert rs.New16(1024, 300).encode_path == "multipass"

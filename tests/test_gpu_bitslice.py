@@ -1,9 +1,10 @@
-"""GPU parity of the bit-sliced encode kernel (csrc/bitslice.hip) against the
-oracle: every geometry compiled in (Makefile BS_CONFIGS), ragged shard sizes
-(a partial last 4 KB tile, a single 64-byte block), several stripes per
-launch, more tiles than workgroups (the persistent loop), strided rows with
-guard bytes past the row end, and verify with tampering in the first and last
-tile of data and parity rows."""
+"""GPU parity of the bit-sliced encode kernel (csrc/bitslice.hip, k_encode_hp)
+against the oracle: m = 32 and m = 16 geometries with full and ragged chunks
+(the per-m tables serve every k up to the chunk cap and every p of the m),
+ragged shard sizes (a partial last 2 KB tile, a single 64-byte block),
+several stripes per launch, more tiles than workgroups (the persistent loop),
+strided rows with guard bytes past the row end, and verify with tampering in
+the first and last tile of data and parity rows."""
 import numpy as np
 import pytest
 
@@ -12,7 +13,11 @@ from oracle import orc
 
 pytestmark = pytest.mark.gpu
 
-BS = [(128, 32), (32, 32), (100, 17)]
+BS = [(128, 32), (32, 32), (100, 17), (130, 32), (192, 32), (1, 17), (64, 16), (9, 9), (192, 16), (33, 12)]
+
+
+def path(p):
+    return "bs16-m32" if p > 16 else "bs16-m16"
 
 
 @pytest.fixture(scope="module")
@@ -24,40 +29,37 @@ def torch():
 
 @pytest.mark.parametrize("k,p", BS)
 def test_bs_path_selected(k, p):
-    assert rs.New16(k, p).encode_path == "bs16-m32"
-
-
-@pytest.fixture(params=["hp", "bs"])
-def kernel(request, monkeypatch):
-    """Both bit-sliced kernels: the half-plane kernel (default for subfield
-    geometries) and the round-1 512-thread kernel (RS_BS_KERNEL=1)."""
-    monkeypatch.setenv("RS_BS_KERNEL", "2" if request.param == "hp" else "1")
-    return request.param
+    assert rs.New16(k, p).encode_path == path(p)
 
 
 @pytest.mark.parametrize("k,p,S,n", [(128, 32, 64, 1), (128, 32, 4096 * 3 + 64 * 5, 1), (128, 32, 8192, 3),
                                      (32, 32, 64 * 37, 2), (32, 32, 4096 * 64, 5), (100, 17, 4096 * 3 + 320, 2),
-                                     (100, 17, 4096, 5), (128, 32, 2048 * 700 + 64 * 3, 2)])
-def test_bs_batch_matches_oracle(torch, kernel, k, p, S, n):
+                                     (100, 17, 4096, 5), (128, 32, 2048 * 700 + 64 * 3, 2),
+                                     (130, 32, 2048 * 5 + 64, 3), (192, 32, 4096, 2), (1, 17, 2048 * 3, 2),
+                                     (64, 16, 64, 1), (64, 16, 2048 * 9 + 64 * 7, 3), (64, 16, 2048 * 1500, 1),
+                                     (9, 9, 2048 * 2 + 192, 4), (192, 16, 4096 + 64, 2), (33, 12, 2048 * 4, 3)])
+def test_bs_batch_matches_oracle(torch, k, p, S, n):
     rng = np.random.default_rng(k * 131 + p * 7 + S + n)
     datas = [rng.integers(0, 256, (k, S), dtype=np.uint8) for _ in range(n)]
     slab = torch.zeros((n, k + p, S), dtype=torch.uint8, device="cuda")
     for j in range(n):
         slab[j, :k] = torch.from_numpy(datas[j]).cuda()
     c = rs.New16(k, p)
-    assert c.encode_path == "bs16-m32"
+    assert c.encode_path == path(p)
     c.encode_dev_batch(slab)
     torch.cuda.synchronize()
     for j in range(n):
         assert np.array_equal(slab[j, k:].cpu().numpy(), orc.encode(16, k, p, datas[j])), f"stripe {j}"
 
 
-def test_bs_special_inputs(torch):
+@pytest.mark.parametrize("k,p", [(128, 32), (64, 16)])
+def test_bs_special_inputs(torch, k, p):
     """All-zero, all-0xFF and single-symbol impulses in every chunk."""
-    k, p, S = 128, 32, 4096
+    S = 4096
     c = rs.New16(k, p)
     cases = [np.zeros((k, S), np.uint8), np.full((k, S), 0xFF, np.uint8)]
-    for r in (0, 31, 32, 77, 127):
+    m = 32 if p > 16 else 16
+    for r in (0, m - 1, m, k // 2 + 13, k - 1):
         d = np.zeros((k, S), np.uint8)
         d[r, 5] = 1
         d[r, 4095] = 0x80
@@ -70,7 +72,7 @@ def test_bs_special_inputs(torch):
         assert np.array_equal(slab[k:].cpu().numpy(), orc.encode(16, k, p, d))
 
 
-@pytest.mark.parametrize("k,p", [(128, 32), (100, 17)])
+@pytest.mark.parametrize("k,p", [(128, 32), (100, 17), (64, 16), (130, 32), (20, 10)])
 def test_bs_strided_rows_and_verify(torch, k, p):
     S = 4096 * 2 + 192
     rng = np.random.default_rng(k + p)
@@ -80,6 +82,7 @@ def test_bs_strided_rows_and_verify(torch, k, p):
     big[:k, :S] = torch.from_numpy(data).cuda()
     view = big[:, :S]
     c = rs.New16(k, p)
+    assert c.encode_path == path(p)
     c.encode_dev(view)
     torch.cuda.synchronize()
     assert np.array_equal(view[k:].cpu().numpy(), ref)
