@@ -275,26 +275,35 @@ struct HpEncoder {
     Half R[RW];   // working rows
     Half A[RW];   // accumulator: coset u (co = U*w + u), rows co + RW*t at A[4u + t]
 
-    // Load rows M*c + RW*w + HR*h + i, i in [I0, I1), of `tile` through a
+    // A tile's stripe and column tile (wave-uniform), decomposed once per tile:
+    // a scalar division costs ~40 instructions of the wave's issue slots.
+    struct Loc {
+        int stripe, ct;
+        bool live;
+    };
+    __device__ __forceinline__ Loc locate(int tile) const {
+        const int tps = a.tiles_per_stripe;
+        const int stripe = tile / tps;
+        return Loc{stripe, tile - stripe * tps, tile < a.ntiles};
+    }
+
+    // Load rows M*c + RW*w + HR*h + i, i in [I0, I1), of tile L through a
     // buffer descriptor over the stripe's data rows: rows past k and bytes past
     // the last row's end read as zero (range check), a tile past the end has
     // an empty range.  Lanes whose block lies past the row end read bytes of
     // the next row; their results are never stored.
     template <int I0, int I1>
-    __device__ __forceinline__ void stage(int tile, int c) {
-        const int tps = a.tiles_per_stripe;
-        const int stripe = tile / tps, ct = tile - stripe * tps;
-        const bool live = tile < a.ntiles;
+    __device__ __forceinline__ void stage(const Loc &L, int c) {
 #ifdef RS_BS_ABL_NOLOAD
         const uint32_t range = 0;
 #else
-        const uint32_t range = live ? a.span : 0u;
+        const uint32_t range = L.live ? a.span : 0u;
 #endif
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(a.data + (live ? (uint64_t)stripe * a.stripe_stride : 0)), 0, (int)range, 0x00020000);
+            (void *)(a.data + (L.live ? (uint64_t)L.stripe * a.stripe_stride : 0)), 0, (int)range, 0x00020000);
         // lane part of the offset (block, half); opaque so that the compiler
         // does not precompute every chunk's offsets
-        uint32_t voff = (uint32_t)ct * TILE + (uint32_t)blk * 64 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
+        uint32_t voff = (uint32_t)L.ct * TILE + (uint32_t)blk * 64 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
         asm volatile("" : "+v"(voff));
 #pragma unroll
         for (int i = I0; i < I1; i++) {
@@ -324,9 +333,9 @@ struct HpEncoder {
 
     // Next chunk's rows i in [I0, I1): chunk C + 1 of this tile, or chunk 0 of the next tile.
     template <int C, int I0, int I1>
-    __device__ __forceinline__ void prefetch(int tile) {
+    __device__ __forceinline__ void prefetch(const Loc &cur, const Loc &nxt) {
         const bool more = C + 1 < nch;  // wave-uniform: one load sequence, no branch
-        stage<I0, I1>(more ? tile : tile + (int)gridDim.x, more ? C + 1 : 0);
+        stage<I0, I1>(more ? cur : nxt, more ? C + 1 : 0);
     }
 
     // The next chunk's loads go out in two halves so that (m = 32) at most
@@ -337,7 +346,7 @@ struct HpEncoder {
     // (Issuing all of them at the chunk start, with 192 VGPRs of data live,
     // spilled to scratch: +8 % HBM traffic.)
     template <int C>
-    __device__ __forceinline__ void chunk(int tile) {
+    __device__ __forceinline__ void chunk(const Loc &cur, const Loc &nxt) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < RW; i++)
@@ -356,14 +365,14 @@ struct HpEncoder {
 #pragma unroll
             for (int q = 0; q < 8; q++) asm volatile("" : "+v"(R[i][q])::"memory");
         __builtin_amdgcn_sched_barrier(0);
-        prefetch<C, 0, HR / 2>(tile);
+        prefetch<C, 0, HR / 2>(cur, nxt);
         __builtin_amdgcn_sched_barrier(0);
         dispatch<4>(w, [&](auto W) { phase1<C, decltype(W)::value>(); });
         lds_barrier();  // every wave has read the previous image
 #pragma unroll
         for (int j = 0; j < RW; j++) hp_put(lbase, RW * w + j, R[j]);
         lds_barrier();
-        prefetch<C, HR / 2, HR>(tile);
+        prefetch<C, HR / 2, HR>(cur, nxt);
         __builtin_amdgcn_sched_barrier(0);
         // IFFT layers r(LR), r(LR+1), one coset at a time
 #pragma unroll
@@ -391,8 +400,8 @@ struct HpEncoder {
     // chunks is never fetched).  Chunk 0 unconditionally: with a branch
     // around it too, the allocator spilled 11-14 VGPRs.
     template <int... Cs>
-    __device__ __forceinline__ void chunks(int tile, std::integer_sequence<int, Cs...>) {
-        ((Cs == 0 || Cs < nch ? (chunk<Cs>(tile), 0) : 0), ...);
+    __device__ __forceinline__ void chunks(const Loc &cur, const Loc &nxt, std::integer_sequence<int, Cs...>) {
+        ((Cs == 0 || Cs < nch ? (chunk<Cs>(cur, nxt), 0) : 0), ...);
     }
 
     // FFT layers r(LR-1) .. r0 on rows RW*W + j.
@@ -410,9 +419,11 @@ struct HpEncoder {
 
     __device__ __forceinline__ void run() {
         int tile = blockIdx.x;
-        stage<0, HR>(tile, 0);
+        Loc cur = locate(tile);
+        stage<0, HR>(cur, 0);
         for (; tile < a.ntiles; tile += gridDim.x) {
-            chunks(tile, std::make_integer_sequence<int, NCH>{});
+            const Loc nxt = locate(tile + (int)gridDim.x);
+            chunks(cur, nxt, std::make_integer_sequence<int, NCH>{});
             // FFT layers r(LR+1), r(LR) in A's layout
 #pragma unroll
             for (int u = 0; u < U; u++) {
@@ -433,11 +444,9 @@ struct HpEncoder {
             hp_swap_halves<HR>(R);
             // parity rows RW*w + HR*h + i < p, through a descriptor over the
             // stripe's parity rows (lanes past the row end store nothing: exec mask)
-            const int tps = a.tiles_per_stripe;
-            const int stripe = tile / tps, ct = tile - stripe * tps;
-            const uint32_t col = (uint32_t)ct * TILE + (uint32_t)blk * 64;
+            const uint32_t col = (uint32_t)cur.ct * TILE + (uint32_t)blk * 64;
             const __amdgpu_buffer_rsrc_t ps = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(a.parity + (uint64_t)stripe * a.stripe_stride), 0, (int)a.pspan, 0x00020000);
+                (void *)(a.parity + (uint64_t)cur.stripe * a.stripe_stride), 0, (int)a.pspan, 0x00020000);
             uint32_t voff = col + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
             asm volatile("" : "+v"(voff));
             uint32_t bad = 0;
@@ -478,6 +487,7 @@ struct HpEncoder {
                 if (m && lane == __ffsll((unsigned long long)m) - 1)
                     __hip_atomic_store(a.mismatch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            cur = nxt;
         }
     }
 };
