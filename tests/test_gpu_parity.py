@@ -295,6 +295,41 @@ def test_byte_range_sharding_on_gpu(torch_dev, bits, k, p, S, world):
     assert torch.equal(broken, whole)
 
 
+def test_c5_shape_world8_byte_split(torch_dev):
+    """The exact C5 configuration (1024 + 256 x 256 KiB, configs[4]) split over
+    8 ranks by byte range, all ranks emulated on this GPU through the batched
+    path bench.py --split bytes uses (dist.encode_sharded_batch: one strided
+    launch per rank over 2 stripes): the reassembled parity equals the
+    whole-stripe encode, and a 256-erasure reconstruct per rank slice restores
+    every row (leopard16.go:778-792 column independence)."""
+    torch = torch_dev
+    from reedsolomon16_amd import dist as rsd
+
+    k, p, S, world, B = 1024, 256, 256 << 10, 8, 2
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0xC5)
+    slab = torch.randint(0, 256, (B, k + p, S), dtype=torch.uint8, device="cuda", generator=g)
+    c = rs.New16(k, p)
+    whole = slab.clone()
+    c.encode_dev_batch(whole)
+    for r in range(world):
+        lo, hi = rsd.byte_range(S, r, world)
+        assert hi - lo == S // world
+        rsd.encode_sharded_batch(slab, r, world, c)
+    torch.cuda.synchronize()
+    assert torch.equal(slab, whole)
+    # one stripe, 256 random erasures, reconstructed slice by slice
+    present = np.ones(k + p, bool)
+    er = np.random.default_rng(0xC5).choice(k + p, p, replace=False)
+    present[er] = False
+    broken = whole[0].clone()
+    broken[torch.from_numpy(er).cuda()] = 0
+    for r in range(world):
+        rsd.reconstruct_sharded(broken, present, r, world, rsd.gpu_reconstruct_fn(c))
+    torch.cuda.synchronize()
+    assert torch.equal(broken, whole[0])
+
+
 # Host-resident pipeline (rs_encode / rs_verify / rs_reconstruct): small
 # segment widths force many segments, a ragged last segment and reuse of every
 # staging slab; rows as one slab (2-D copies) and as scattered arrays
