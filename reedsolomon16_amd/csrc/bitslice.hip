@@ -267,6 +267,10 @@ struct HpEncoder {
     static constexpr int U = M / 16;       // cosets per wave
     static constexpr int NCH = TW::NCH;    // chunks compiled in (k <= NCH * m)
     static constexpr int TILE = 2048;      // column bytes per tile (32 blocks)
+#ifndef RS_HP_PF1  // rows of the next chunk issued before phase 1 (m = 32)
+#define RS_HP_PF1 2
+#endif
+    static constexpr int PF1 = LOGM == 5 ? RS_HP_PF1 : HR / 2;
     static_assert(LOGM == 4 || LOGM == 5, "m = 16 or 32");
     const BsArgs &a;
     uint32_t lbase;  // this lane's LDS byte address of row 0, quad 0
@@ -303,7 +307,13 @@ struct HpEncoder {
             (void *)(a.data + (L.live ? (uint64_t)L.stripe * a.stripe_stride : 0)), 0, (int)range, 0x00020000);
         // lane part of the offset (block, half); opaque so that the compiler
         // does not precompute every chunk's offsets
+#ifdef RS_HP_ABL_COALESCED  // ablation: same bytes, lane-contiguous 16-byte pieces (wrong layout)
+        uint32_t voff = (uint32_t)L.ct * TILE + (uint32_t)blk * 16 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
+        constexpr uint32_t QS = 512;
+#else
         uint32_t voff = (uint32_t)L.ct * TILE + (uint32_t)blk * 64 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
+        constexpr uint32_t QS = 16;
+#endif
         asm volatile("" : "+v"(voff));
 #pragma unroll
         for (int i = I0; i < I1; i++) {
@@ -311,7 +321,7 @@ struct HpEncoder {
             const uint32_t soff = (uint32_t)(M * c + RW * w + i) * (uint32_t)a.row_stride;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * 16, soff, 0);
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * QS, soff, 0);
                 uint32_t *d = q < 2 ? &St[i][q * 4] : &St[HR + i][(q - 2) * 4];
                 d[0] = x[0], d[1] = x[1], d[2] = x[2], d[3] = x[3];
             }
@@ -365,14 +375,14 @@ struct HpEncoder {
 #pragma unroll
             for (int q = 0; q < 8; q++) asm volatile("" : "+v"(R[i][q])::"memory");
         __builtin_amdgcn_sched_barrier(0);
-        prefetch<C, 0, HR / 2>(cur, nxt);
+        prefetch<C, 0, PF1>(cur, nxt);
         __builtin_amdgcn_sched_barrier(0);
         dispatch<4>(w, [&](auto W) { phase1<C, decltype(W)::value>(); });
         lds_barrier();  // every wave has read the previous image
 #pragma unroll
         for (int j = 0; j < RW; j++) hp_put(lbase, RW * w + j, R[j]);
         lds_barrier();
-        prefetch<C, HR / 2, HR>(cur, nxt);
+        prefetch<C, PF1, HR>(cur, nxt);
         __builtin_amdgcn_sched_barrier(0);
         // IFFT layers r(LR), r(LR+1), one coset at a time
 #pragma unroll
@@ -447,7 +457,13 @@ struct HpEncoder {
             const uint32_t col = (uint32_t)cur.ct * TILE + (uint32_t)blk * 64;
             const __amdgpu_buffer_rsrc_t ps = __builtin_amdgcn_make_buffer_rsrc(
                 (void *)(a.parity + (uint64_t)cur.stripe * a.stripe_stride), 0, (int)a.pspan, 0x00020000);
+#ifdef RS_HP_ABL_COALESCED
+            uint32_t voff = (uint32_t)cur.ct * TILE + (uint32_t)blk * 16 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
+            constexpr uint32_t QS = 512;
+#else
             uint32_t voff = col + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
+            constexpr uint32_t QS = 16;
+#endif
             asm volatile("" : "+v"(voff));
             uint32_t bad = 0;
             if (col < a.S) {
@@ -469,13 +485,13 @@ struct HpEncoder {
                         const u32x4 v = k < 2 ? u32x4{R[i][o], R[i][o + 1], R[i][o + 2], R[i][o + 3]}
                                               : u32x4{R[HR + i][o], R[HR + i][o + 1], R[HR + i][o + 2], R[HR + i][o + 3]};
                         if constexpr (VERIFY) {
-                            const u32x4 old = __builtin_amdgcn_raw_buffer_load_b128(ps, voff + k * 16, soff, 0);
+                            const u32x4 old = __builtin_amdgcn_raw_buffer_load_b128(ps, voff + k * QS, soff, 0);
                             bad |= (old[0] ^ v[0]) | (old[1] ^ v[1]) | (old[2] ^ v[2]) | (old[3] ^ v[3]);
                         } else {
 #if defined(RS_BS_ABL_NOSTORE)
                             asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
 #else
-                            __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * 16, soff, 0);
+                            __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * QS, soff, 0);
 #endif
                         }
                     }

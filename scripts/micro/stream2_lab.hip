@@ -16,14 +16,14 @@ constexpr int K = 128, P = 32, NST = 16;
 constexpr size_t S = 1 << 20;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int LAYOUT, int DEPTH, bool BAR>
+template <int LAYOUT, int DEPTH, bool BAR, bool SPLIT = false>
 __global__ void __launch_bounds__(256, 2) k_stream(uint8_t *base, uint32_t *sink, uint32_t RS, uint32_t TS, uint64_t SS) {
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, blk = lane & 31;
     constexpr int TPS = S / 2048, NT = TPS * NST;
     uint32_t St[DEPTH][64];
     uint32_t acc[64];
-    auto stage = [&](int tile, int c, uint32_t (&d)[64]) {
+    auto stage = [&](int tile, int c, uint32_t (&d)[64], int i0 = 0, int i1 = 4) {
         const int stripe = tile / TPS, ct = tile % TPS;
         const bool live = tile < NT;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -36,6 +36,7 @@ __global__ void __launch_bounds__(256, 2) k_stream(uint8_t *base, uint32_t *sink
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
+                if (i < i0 || i >= i1) continue;
                 uint32_t so, vo;
                 if (LAYOUT == 0) { so = (uint32_t)(32 * c + 8 * w + i) * RS; vo = voff + q * 16; }
                 else { so = (uint32_t)(32 * c + 8 * w + i + 4 * (q >> 1)) * RS; vo = voff + (q & 1) * 1024; }
@@ -60,7 +61,14 @@ __global__ void __launch_bounds__(256, 2) k_stream(uint8_t *base, uint32_t *sink
 #pragma unroll
             for (int j = 0; j < 64; j++) asm volatile("" : "+v"(acc[j])::"memory");
             const int nc = c + DEPTH;  // chunk index that reuses this slot
-            stage(nc < 4 ? tile : tile + gridDim.x, nc % 4, cur);
+            if (SPLIT) {
+                stage(nc < 4 ? tile : tile + gridDim.x, nc % 4, cur, 0, 2);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_s_barrier();
+                stage(nc < 4 ? tile : tile + gridDim.x, nc % 4, cur, 2, 4);
+            } else {
+                stage(nc < 4 ? tile : tile + gridDim.x, nc % 4, cur);
+            }
             if (BAR) {
                 __builtin_amdgcn_s_barrier();
                 __builtin_amdgcn_s_barrier();
@@ -188,6 +196,12 @@ int main() {
     const uint32_t RS = (uint32_t)S, TS = 2048;
     const uint64_t SS = (K + P) * S;
     rep("regs d1", timeit([&] { hipLaunchKernelGGL((k_stream<0, 1, false>), dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
+    rep("regs d1 bar", timeit([&] { hipLaunchKernelGGL((k_stream<0, 1, true>), dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
+    rep("regs d1 split", timeit([&] { hipLaunchKernelGGL((k_stream<0, 1, false, true>), dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
+    rep("regs d2", timeit([&] { hipLaunchKernelGGL((k_stream<0, 2, false>), dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
+    rep("contig d1", timeit([&] { hipLaunchKernelGGL((k_stream<1, 1, false>), dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
+    rep("contig d1 bar", timeit([&] { hipLaunchKernelGGL((k_stream<1, 1, true>), dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
+    rep("regs d1 grid1024", timeit([&] { hipLaunchKernelGGL((k_stream<0, 1, false>), dim3(1024), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
     {
         const size_t half = bytes / 2, n16 = half / 16;
         for (int g : {2048, 4096, 8192, 16384}) {
