@@ -305,14 +305,19 @@ struct F16S : F16<W_> {
 };
 
 // ---------------------------------------------------------------- butterflies
+#ifdef RS_LDS_ABL_NOMUL  // ablation (performance experiments only): table-driven butterflies are XOR-only
+#define RS_TW_LIVE(t) false
+#else
+#define RS_TW_LIVE(t) ((t)[F::LOGIDX] != F::MOD)
+#endif
 template <class F>
 __device__ __forceinline__ void ifft2(typename F::Vec &x, typename F::Vec &y, const uint32_t *__restrict__ t) {
     F::xor_into(y, x);
-    if (t[F::LOGIDX] != F::MOD) F::mul_add(x, y, t);
+    if (RS_TW_LIVE(t)) F::mul_add(x, y, t);
 }
 template <class F>
 __device__ __forceinline__ void fft2(typename F::Vec &x, typename F::Vec &y, const uint32_t *__restrict__ t) {
-    if (t[F::LOGIDX] != F::MOD) F::mul_add(x, y, t);
+    if (RS_TW_LIVE(t)) F::mul_add(x, y, t);
     F::xor_into(y, x);
 }
 // Branch-free forms for the fused register kernels: a zero twiddle is shipped
@@ -1287,7 +1292,9 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
             L::put(lds, ry, u, y);
         }
     }
+#ifndef RS_LDS_ABL_NOBAR  // ablation: wrong results, measures the barrier cost
     __syncthreads();
+#endif
 }
 
 // Full transform over 2^LOGN LDS rows with the reference's pass structure
@@ -1340,12 +1347,19 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         const int r = it / U, u = it - r * U;
         V v = F::zero();
         const uint8_t *src = a.src[r];
+#ifdef RS_REC_ABL_NOSCALE  // ablation (performance experiments only): load without the multiply
+        if (src && L::valid(tile, a.S, u)) v = F::load(src + tile, u);
+#else
         if (src && L::valid(tile, a.S, u)) F::mul_add(v, F::load(src + tile, u), a.tw_in + (uint64_t)r * F::TWD);
+#endif
         L::put(lds, r, u, v);
     }
     __syncthreads();
+#ifndef RS_REC_ABL_NOIFFT
     lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft);
+#endif
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
+#ifndef RS_REC_ABL_NODERIV
     {
         V o[K];
 #pragma unroll
@@ -1369,6 +1383,8 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         }
         __syncthreads();
     }
+#endif
+#ifndef RS_REC_ABL_NOFFT
     if (a.prune) {
         uint32_t need[8];
 #pragma unroll
@@ -1377,6 +1393,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     } else {
         lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft);
     }
+#endif
     // reveal: shard = work[pos] * (modulus - errLocs[pos])
     for (int it = threadIdx.x; it < a.nd * U; it += 256) {
         const int j = it / U, u = it - j * U;
