@@ -1262,11 +1262,11 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
     if (radix == 4) {
         const int items = groups_active * dist * U;
         const int ld = __builtin_ctz((unsigned)dist);  // dist is a power of two: no integer division
-        for (int it = threadIdx.x; it < items; it += 256) {
+        auto group = [&](int it, int g) {
             const int q = it / U, u = it - q * U;
-            const int g = q >> ld, j = q & (dist - 1);
+            const int j = q & (dist - 1);
             const int i = g * 4 * dist + j;
-            if (!INV && need && !rows_needed(*need, g * 4 * dist, 4 * dist)) continue;
+            if (!INV && need && !rows_needed(*need, g * 4 * dist, 4 * dist)) return;
             const uint32_t *t = tw + (uint64_t)g * 3 * F::TWD;
             V x0 = L::get(lds, i, u), x1 = L::get(lds, i + dist, u), x2 = L::get(lds, i + 2 * dist, u),
               x3 = L::get(lds, i + 3 * dist, u);
@@ -1276,6 +1276,18 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
             L::put(lds, i + dist, u, x1);
             L::put(lds, i + 2 * dist, u, x2);
             L::put(lds, i + 3 * dist, u, x3);
+        };
+#ifndef RS_LDS_VECTOR_TW
+        if (dist * U >= 64) {
+            // A wave's 64 items (aligned) lie in one group: the group index is
+            // wave-uniform, so its twiddle tables come in by scalar loads and
+            // the zero-twiddle test is a scalar branch.
+            for (int it = threadIdx.x; it < items; it += 256)
+                group(it, __builtin_amdgcn_readfirstlane((it / U) >> ld));
+        } else
+#endif
+        {
+            for (int it = threadIdx.x; it < items; it += 256) group(it, (it / U) >> ld);
         }
     } else {
         // inverse: pairs (j, j + dist), j < dist, one twiddle; forward: dist 1, pairs (2g, 2g+1), twiddle g
