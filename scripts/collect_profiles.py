@@ -83,6 +83,7 @@ def main():
         hbm = 2 * fetch + write
         traffic[p] = {"hbm_bytes_per_launch": round(hbm), "fetch_size_bytes": round(fetch),
                       "write_size_bytes": round(write), "launches": len(fk),
+                      "stripes": bench["config"].get("stripes_per_step", 16),
                       "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE = half of streamed reads)",
                       "round": tag}
         lines.append(f"{p}: FETCH_SIZE {fetch/1e6:.2f} MB (x2 = {2*fetch/1e6:.2f}), WRITE_SIZE {write/1e6:.2f} MB, "
