@@ -20,6 +20,37 @@
 
 namespace rs {
 
+// Twiddle slot of one butterfly of the reference schedule (gf_host.cpp
+// ifft_passes / fft_passes order), by layer and the lower row of its pair.
+constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
+// IFFT: radix-4 passes at dist 1, 4, 16, ... then a radix-2 pass if logm is
+// odd.  A radix-4 group's slots are (m01, m02, m23): layer log2(dist) pairs
+// rows with m01 (second bit of row/dist clear) or m23, layer log2(dist)+1
+// pairs them with m02.
+constexpr int ifft_slot(int logm, int layer, int row) {
+    int off = 0;
+    for (int dist = 1; dist * 4 <= (1 << logm); dist *= 4) {
+        const int l0 = ilog2c(dist), g = row / (4 * dist);
+        if (layer == l0 + 1) return off + 3 * g + 1;
+        if (layer == l0) return off + 3 * g + (((row / dist) & 2) ? 2 : 0);
+        off += 3 * ((1 << logm) / (4 * dist));
+    }
+    return off;
+}
+// FFT: radix-4 passes at dist m/4, m/16, ... (layer log2(dist)+1 first, with
+// m02), then a radix-2 pass over layer 0 if logm is odd (slot per row pair).
+constexpr int fft_slot(int logm, int layer, int row) {
+    const int M = 1 << logm;
+    int off = 0, dist4 = M;
+    for (int dist = M >> 2; dist != 0; dist4 = dist, dist >>= 2) {
+        const int l0 = ilog2c(dist), g = row / dist4;
+        if (layer == l0 + 1) return off + 3 * g + 1;
+        if (layer == l0) return off + 3 * g + (((row / dist) & 2) ? 2 : 0);
+        off += 3 * (M / dist4);
+    }
+    return off + row / 2;
+}
+
 enum : int { OP_IFFT = 0, OP_FFT = 1, OP_FFTX = 2 };
 struct BOp {
     int x, y, slot, kind;

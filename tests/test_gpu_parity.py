@@ -589,3 +589,69 @@ def test_encode_async_stream_of_blocks():
     t = c.encode_async(sh)
     t.wait()
     assert np.array_equal(np.stack(sh[k:]), orc.encode(16, k, p, np.stack(sh[:k])))
+
+
+# Radix-16 kernels for 256-point transforms (k_rec_r16: reconstruct with
+# n = 256; k_enc_r16: encode with m = 256).  RS_R16=1 forces them at these
+# small sizes (they run automatically from 512 workgroups up, e.g. C4 / C5),
+# RS_R16=0 runs the radix-4 LDS kernels on the same inputs.
+@pytest.mark.parametrize("r16", ["1", "0"])
+@pytest.mark.parametrize("k,p,S", [(128, 32, 2048 + 64), (100, 100, 512), (190, 33, 256), (129, 64, 320)])
+def test_radix16_reconstruct(monkeypatch, r16, k, p, S):
+    monkeypatch.setenv("RS_R16", r16)
+    rng = np.random.default_rng(k * 3 + p + S)
+    data = rand_data(rng, k, S)
+    par, c = gpu_encode(16, k, p, data)
+    full = [data[i].copy() for i in range(k)] + [par[i].copy() for i in range(p)]
+    o = orc.Oracle(16, k, p)
+    patterns = [list(range(p)), list(range(k, k + p)), [0], [k + p - 1], [3, k + 1],
+                rng.choice(k + p, p, replace=False).tolist(), rng.choice(k + p, max(1, p // 4), replace=False).tolist()]
+    for er in patterns:
+        er = set(er)
+        sh = [None if i in er else full[i].copy() for i in range(k + p)]
+        c.reconstruct(sh)
+        e, ref = o.reconstruct([None if i in er else full[i].copy() for i in range(k + p)])
+        assert e == 0
+        for i in range(k + p):
+            assert np.array_equal(sh[i], full[i]), f"shard {i} (erased={i in er})"
+            assert np.array_equal(sh[i], ref[i]), f"shard {i} vs oracle"
+
+
+@pytest.mark.parametrize("r16", ["1", "0"])
+def test_radix16_reconstruct_full_field(monkeypatch, r16):
+    """k_rec_r16<F16<2>> (transforms outside subfield coordinates, RS_NO_SUB=1)."""
+    monkeypatch.setenv("RS_R16", r16)
+    monkeypatch.setenv("RS_NO_SUB", "1")
+    k, p, S = 128, 32, 1024
+    rng = np.random.default_rng(77)
+    data = rand_data(rng, k, S)
+    par, c = gpu_encode(16, k, p, data)
+    full = [data[i].copy() for i in range(k)] + [par[i].copy() for i in range(p)]
+    er = set(rng.choice(k + p, p, replace=False).tolist())
+    sh = [None if i in er else full[i].copy() for i in range(k + p)]
+    c.reconstruct(sh)
+    for i in range(k + p):
+        assert np.array_equal(sh[i], full[i])
+
+
+@pytest.mark.parametrize("r16", ["1", "0"])
+@pytest.mark.parametrize("k,p,S", [(300, 256, 256 + 64), (257, 129, 256), (1024, 256, 512), (200, 200, 64)])
+def test_radix16_encode_verify(torch_dev, monkeypatch, r16, k, p, S):
+    monkeypatch.setenv("RS_R16", r16)
+    torch = torch_dev
+    rng = np.random.default_rng(k + p * 5 + S)
+    B = 3
+    datas = [rand_data(rng, k, S) for _ in range(B)]
+    slab = torch.zeros((B, k + p, S), dtype=torch.uint8, device="cuda")
+    for j in range(B):
+        slab[j, :k] = torch.from_numpy(datas[j]).cuda()
+    c = rs.New16(k, p)
+    assert c.encode_path == "lds-m256"
+    c.encode_dev_batch(slab)
+    torch.cuda.synchronize()
+    for j in range(B):
+        assert np.array_equal(slab[j, k:].cpu().numpy(), orc.encode(16, k, p, datas[j])), f"stripe {j}"
+    one = slab[1].clone()
+    assert c.verify_dev(one)
+    one[k + p - 1, S - 1] ^= 1
+    assert not c.verify_dev(one)
