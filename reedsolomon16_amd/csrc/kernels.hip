@@ -1490,6 +1490,9 @@ __global__ void __launch_bounds__(256) k_enc_lds(EncodeArgs a) {
 // groups x 16 units.  LDS row: [lo bytes of units 0..15][hi bytes], stride
 // 264 B (66 dwords: rows 16 apart land 32 banks apart, so pass A's ds_read_b64
 // lane groups are conflict-free).
+#ifndef RS_R16_SCHED
+#define RS_R16_SCHED 2
+#endif
 struct R16 {
     typedef F16<2> F;  // full-field unit: loads, stores, scale-in / reveal tables
     typedef F::Vec V;
@@ -1537,9 +1540,17 @@ __device__ __forceinline__ void r16_layers(typename FT::Vec (&x)[16], const uint
             } else {
                 t = tw + (INV ? ifft_slot(8, l, row0 + a) : fft_slot(8, l, row0 + a)) * FT::TWD;
             }
-            if constexpr (INV) ifft2<FT>(x[a], x[a + (1 << l)], t);
-            else fft2<FT>(x[a], x[a + (1 << l)], t);
+            // branch-free: a zero twiddle's table is all zeros (product 0), and a
+            // data-dependent branch per butterfly would serialize the table loads
+            if constexpr (INV) ifft2m<FT>(x[a], x[a + (1 << l)], t);
+            else fft2m<FT>(x[a], x[a + (1 << l)], t);
+#if RS_R16_SCHED == 1
+            __builtin_amdgcn_sched_barrier(0);  // one butterfly per scheduling region
+#endif
         });
+#if RS_R16_SCHED == 2
+        __builtin_amdgcn_sched_barrier(0);  // one layer per scheduling region
+#endif
     });
 }
 
@@ -1696,16 +1707,21 @@ __global__ void __launch_bounds__(256, 2) k_enc_r16(EncodeArgs a) {
     if constexpr (VERIFY) flag_mismatch(a.mismatch, bad != 0);
 }
 
-// RS_R16=0 disables the radix-16 kernels, RS_R16=1 forces them for every
-// eligible launch (the parity tests run them at small sizes); unset: used
-// when the launch has at least kLdsMinGrid workgroups.
+// Opt-in (RS_R16=1): measured on MI355X (scripts/gpu_r16.sh) the radix-16
+// kernels are slower than the radix-4 LDS kernels -- C4 312 vs 193 us, C5
+// 266 vs 262 us per launch.  Two LDS round trips instead of nine do not pay
+// for what the register-resident passes cost: 8-symbol units (16 rows x 8
+// symbols fit the registers; the radix-4 kernels use 16-symbol units) double
+// the twiddle-table loads per symbol, pass A's per-group tables are
+// lane-varying vector loads, and only 2 workgroups fit a CU's LDS (8 waves,
+// against 16) to hide their latency; the m = 256 encode also spills.
 int r16_mode() {
     const char *e = getenv("RS_R16");
     return !e ? -1 : e[0] == '1' ? 1 : 0;
 }
 bool r16_pick(uint64_t groups) {
-    const int m = r16_mode();
-    return m < 0 ? groups >= kLdsMinGrid : m == 1;
+    (void)groups;
+    return r16_mode() == 1;
 }
 
 template <class F, class FT, int LOGN>

@@ -592,9 +592,9 @@ def test_encode_async_stream_of_blocks():
 
 
 # Radix-16 kernels for 256-point transforms (k_rec_r16: reconstruct with
-# n = 256; k_enc_r16: encode with m = 256).  RS_R16=1 forces them at these
-# small sizes (they run automatically from 512 workgroups up, e.g. C4 / C5),
-# RS_R16=0 runs the radix-4 LDS kernels on the same inputs.
+# n = 256; k_enc_r16: encode with m = 256), opt-in with RS_R16=1 (slower than
+# the radix-4 LDS kernels on MI355X); RS_R16=0 runs the radix-4
+# LDS kernels on the same inputs.
 @pytest.mark.parametrize("r16", ["1", "0"])
 @pytest.mark.parametrize("k,p,S", [(128, 32, 2048 + 64), (100, 100, 512), (190, 33, 256), (129, 64, 320)])
 def test_radix16_reconstruct(monkeypatch, r16, k, p, S):
