@@ -343,21 +343,38 @@ __device__ __forceinline__ void fft2x(typename F::Vec &x, typename F::Vec &y) {
 }
 
 // Slot order of a radix-4 group: t[0] = m01, t[1] = m02, t[2] = m23 (each F::TWD dwords).
-template <class F>
+// BF: branch-free multiplies (a zero twiddle's table is all zeros), for
+// lane-varying tables, where a per-lane zero test would make every multiply
+// wait for its table load.
+template <class F, bool BF = false>
 __device__ __forceinline__ void ifft4(typename F::Vec &x0, typename F::Vec &x1, typename F::Vec &x2,
                                       typename F::Vec &x3, const uint32_t *__restrict__ t) {
-    ifft2<F>(x0, x1, t);               // m01
-    ifft2<F>(x2, x3, t + 2 * F::TWD);  // m23
-    ifft2<F>(x0, x2, t + F::TWD);      // m02
-    ifft2<F>(x1, x3, t + F::TWD);
+    if constexpr (BF) {
+        ifft2m<F>(x0, x1, t);
+        ifft2m<F>(x2, x3, t + 2 * F::TWD);
+        ifft2m<F>(x0, x2, t + F::TWD);
+        ifft2m<F>(x1, x3, t + F::TWD);
+    } else {
+        ifft2<F>(x0, x1, t);               // m01
+        ifft2<F>(x2, x3, t + 2 * F::TWD);  // m23
+        ifft2<F>(x0, x2, t + F::TWD);      // m02
+        ifft2<F>(x1, x3, t + F::TWD);
+    }
 }
-template <class F>
+template <class F, bool BF = false>
 __device__ __forceinline__ void fft4(typename F::Vec &x0, typename F::Vec &x1, typename F::Vec &x2, typename F::Vec &x3,
                                      const uint32_t *__restrict__ t) {
-    fft2<F>(x0, x2, t + F::TWD);  // m02
-    fft2<F>(x1, x3, t + F::TWD);
-    fft2<F>(x0, x1, t);               // m01
-    fft2<F>(x2, x3, t + 2 * F::TWD);  // m23
+    if constexpr (BF) {
+        fft2m<F>(x0, x2, t + F::TWD);
+        fft2m<F>(x1, x3, t + F::TWD);
+        fft2m<F>(x0, x1, t);
+        fft2m<F>(x2, x3, t + 2 * F::TWD);
+    } else {
+        fft2<F>(x0, x2, t + F::TWD);  // m02
+        fft2<F>(x1, x3, t + F::TWD);
+        fft2<F>(x0, x1, t);               // m01
+        fft2<F>(x2, x3, t + 2 * F::TWD);  // m23
+    }
 }
 
 // Twiddle slots of an IFFT of size 2^logm (must match gf_host.cpp ifft_passes).
@@ -1176,6 +1193,10 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 // tile must cover whole 64-byte blocks (low bytes [0,32), high bytes
 // [32,64)), so W = 1 (32-byte tiles) is invalid: the parity tests reject it.
 constexpr uint64_t kLdsMinGrid = 512;
+#ifndef RS_LDS_BRANCHFREE
+#define RS_LDS_BRANCHFREE 1
+#endif
+constexpr bool kLdsBranchFree = RS_LDS_BRANCHFREE;  // lane-varying passes: branch-free multiplies
 #ifndef RS_LDS_PAD
 #define RS_LDS_PAD 16  // LDS row padding of the LDS-resident kernels (bytes)
 #endif
@@ -1265,7 +1286,8 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
     if (radix == 4) {
         const int items = groups_active * dist * U;
         const int ld = __builtin_ctz((unsigned)dist);  // dist is a power of two: no integer division
-        auto group = [&](int it, int g) {
+        auto group = [&](int it, int g, auto bf) {
+            constexpr bool BF = decltype(bf)::value;
             const int q = it / U, u = it - q * U;
             const int j = q & (dist - 1);
             const int i = g * 4 * dist + j;
@@ -1273,8 +1295,8 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
             const uint32_t *t = tw + (uint64_t)g * 3 * F::TWD;
             V x0 = L::get(lds, i, u), x1 = L::get(lds, i + dist, u), x2 = L::get(lds, i + 2 * dist, u),
               x3 = L::get(lds, i + 3 * dist, u);
-            if constexpr (INV) ifft4<F>(x0, x1, x2, x3, t);
-            else fft4<F>(x0, x1, x2, x3, t);
+            if constexpr (INV) ifft4<F, BF>(x0, x1, x2, x3, t);
+            else fft4<F, BF>(x0, x1, x2, x3, t);
             L::put(lds, i, u, x0);
             L::put(lds, i + dist, u, x1);
             L::put(lds, i + 2 * dist, u, x2);
@@ -1286,11 +1308,11 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
             // wave-uniform, so its twiddle tables come in by scalar loads and
             // the zero-twiddle test is a scalar branch.
             for (int it = threadIdx.x; it < items; it += 256)
-                group(it, __builtin_amdgcn_readfirstlane((it / U) >> ld));
+                group(it, __builtin_amdgcn_readfirstlane((it / U) >> ld), std::false_type{});
         } else
 #endif
         {
-            for (int it = threadIdx.x; it < items; it += 256) group(it, (it / U) >> ld);
+            for (int it = threadIdx.x; it < items; it += 256) group(it, (it / U) >> ld, std::bool_constant<kLdsBranchFree>{});
         }
     } else {
         // inverse: pairs (j, j + dist), j < dist, one twiddle; forward: dist 1, pairs (2g, 2g+1), twiddle g
