@@ -1272,14 +1272,38 @@ __device__ __forceinline__ bool rows_needed(const uint32_t (&w)[8], int lo, int 
     return ((word >> (lo & 31)) & ((1u << cnt) - 1)) != 0;
 }
 
+// Row sources / sinks of a pass: the LDS image by default; the first pass of
+// a transform may read its rows from HBM (LdsIn replaced by a loader) and the
+// last may write them out (to HBM, or XOR them into the encoder's
+// accumulator), so the tile is not staged through LDS an extra time.
+template <class F>
+struct LdsIO {
+    uint8_t *lds;
+    __device__ typename F::Vec operator()(int row, int u) const { return LTile<F>::get(lds, row, u); }
+    __device__ void operator()(int row, int u, const typename F::Vec &v) const { LTile<F>::put(lds, row, u, v); }
+};
+
+template <class T> struct IsLdsIO : std::false_type {};
+template <class F> struct IsLdsIO<LdsIO<F>> : std::true_type {};
+
+template <class Fn, int... Is>
+__device__ __forceinline__ void cfor_impl(Fn &&f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class Fn>
+__device__ __forceinline__ void cfor(Fn &&f) {
+    cfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 // One radix-4 pass (rows i, i+d, i+2d, i+3d; twiddles m01, m02, m23 at
-// tw + 3*g) over the active groups, or a radix-2 pass, on the LDS rows.
+// tw + 3*g) over the active groups, or a radix-2 pass.  in(row, u) supplies
+// the rows, out(row, u, v) takes the results.
 // need (forward passes only): skip groups none of whose rows is read later --
 // the pruning of errorBitfield.fftDIT (leopard16.go:1215-1252); the rows that
 // are read come out identical.
-template <class F, bool INV>
-__device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int groups_active,
-                                         const uint32_t *__restrict__ tw, const uint32_t (*need)[8] = nullptr) {
+template <class F, bool INV, class In, class Out>
+__device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active, const uint32_t *__restrict__ tw,
+                                         const uint32_t (*need)[8], const In &in, const Out &out) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
     constexpr int U = L::U;
@@ -1293,14 +1317,13 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
             const int i = g * 4 * dist + j;
             if (!INV && need && !rows_needed(*need, g * 4 * dist, 4 * dist)) return;
             const uint32_t *t = tw + (uint64_t)g * 3 * F::TWD;
-            V x0 = L::get(lds, i, u), x1 = L::get(lds, i + dist, u), x2 = L::get(lds, i + 2 * dist, u),
-              x3 = L::get(lds, i + 3 * dist, u);
+            V x0 = in(i, u), x1 = in(i + dist, u), x2 = in(i + 2 * dist, u), x3 = in(i + 3 * dist, u);
             if constexpr (INV) ifft4<F, BF>(x0, x1, x2, x3, t);
             else fft4<F, BF>(x0, x1, x2, x3, t);
-            L::put(lds, i, u, x0);
-            L::put(lds, i + dist, u, x1);
-            L::put(lds, i + 2 * dist, u, x2);
-            L::put(lds, i + 3 * dist, u, x3);
+            out(i, u, x0);
+            out(i + dist, u, x1);
+            out(i + 2 * dist, u, x2);
+            out(i + 3 * dist, u, x3);
         };
 #ifndef RS_LDS_VECTOR_TW
         if (dist * U >= 64) {
@@ -1322,11 +1345,11 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
             const int rx = INV ? q : 2 * q, ry = INV ? q + dist : 2 * q + 1;
             if (!INV && need && !rows_needed(*need, 2 * q, 2)) continue;
             const uint32_t *t = INV ? tw : tw + (uint64_t)q * F::TWD;
-            V x = L::get(lds, rx, u), y = L::get(lds, ry, u);
+            V x = in(rx, u), y = in(ry, u);
             if constexpr (INV) ifft2<F>(x, y, t);
             else fft2<F>(x, y, t);
-            L::put(lds, rx, u, x);
-            L::put(lds, ry, u, y);
+            out(rx, u, x);
+            out(ry, u, y);
         }
     }
 #ifndef RS_LDS_ABL_NOBAR  // ablation: wrong results, measures the barrier cost
@@ -1335,42 +1358,62 @@ __device__ __forceinline__ void lds_pass(uint8_t *lds, int dist, int radix, int 
 }
 
 // Full transform over 2^LOGN LDS rows with the reference's pass structure
-// (gf_host.cpp ifft_passes / fft_passes) and its mtrunc group skipping.
+// (gf_host.cpp ifft_passes / fft_passes) and its mtrunc group skipping.  The
+// first pass reads through `in`, the last writes through `out`.  A first pass
+// that does not read the LDS image runs every group (rows past mtrunc come in
+// as zero, and zero rows transform to zero rows): later passes read those rows.
+template <class F, bool INV, int LOGN, class In, class Out>
+__device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
+                                              const uint32_t (*need)[8], const In &in, const Out &out) {
+    constexpr int N = 1 << LOGN, NP4 = LOGN / 2, NP = NP4 + (LOGN & 1);
+    const LdsIO<F> lio{lds};
+    cfor<NP>([&](auto PI) {
+        constexpr int p = decltype(PI)::value;
+        constexpr bool radix4 = p < NP4;
+        // IFFT: radix-4 passes at dist 4^p (groups N / (4 dist)), then radix-2 at dist N/2;
+        // FFT: radix-4 passes at dist N / 4^(p+1) (groups 4^p), then radix-2 at dist 1
+        constexpr int dist = INV ? (1 << (2 * p)) : (radix4 ? N >> (2 * (p + 1)) : 1);
+        constexpr int groups = radix4 ? N / (4 * dist) : 1;
+        constexpr int slot = [] {
+            int sl = 0;
+            for (int q = 0; q < p; q++) sl += 3 * (INV ? N / (4 << (2 * q)) : (1 << (2 * q)));
+            return sl;
+        }();
+        int active;
+        if constexpr (radix4) {
+            active = (mtrunc + 4 * dist - 1) / (4 * dist);
+            if (active > groups) active = groups;
+        } else {
+            active = INV ? 1 : (mtrunc + 1) / 2 < N / 2 ? (mtrunc + 1) / 2 : N / 2;
+        }
+        const uint32_t *t = tw + (uint64_t)slot * F::TWD;
+        auto run = [&](const auto &pin, const auto &pout) {
+            lds_pass<F, INV>(dist, radix4 ? 4 : 2, active, t, INV ? nullptr : need, pin, pout);
+        };
+        if constexpr (p == 0 && !IsLdsIO<In>::value) {
+            if constexpr (radix4) active = groups;
+            else active = INV ? 1 : N / 2;
+            if constexpr (p == NP - 1) run(in, out);
+            else run(in, lio);
+        } else if constexpr (p == NP - 1) {
+            run(lio, out);
+        } else {
+            run(lio, lio);
+        }
+    });
+}
 template <class F, bool INV, int LOGN>
 __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
                                               const uint32_t (*need)[8] = nullptr) {
-    constexpr int N = 1 << LOGN;
-    int slot = 0;
-    if constexpr (INV) {
-        int dist = 1;
-        for (; dist * 4 <= N; dist *= 4) {
-            const int groups = N / (4 * dist);
-            int active = (mtrunc + 4 * dist - 1) / (4 * dist);
-            if (active > groups) active = groups;
-            lds_pass<F, true>(lds, dist, 4, active, tw + (uint64_t)slot * F::TWD);
-            slot += 3 * groups;
-        }
-        if (dist < N) lds_pass<F, true>(lds, dist, 2, 1, tw + (uint64_t)slot * F::TWD);
-    } else {
-        int dist = N / 4;
-        for (; dist != 0; dist /= 4) {
-            const int groups = N / (4 * dist);
-            int active = (mtrunc + 4 * dist - 1) / (4 * dist);
-            if (active > groups) active = groups;
-            lds_pass<F, false>(lds, dist, 4, active, tw + (uint64_t)slot * F::TWD, need);
-            slot += 3 * groups;
-        }
-        if (LOGN & 1) {
-            int active = (mtrunc + 1) / 2;
-            if (active > N / 2) active = N / 2;
-            lds_pass<F, false>(lds, 1, 2, active, tw + (uint64_t)slot * F::TWD, need);
-        }
-    }
+    const LdsIO<F> lio{lds};
+    lds_transform<F, INV, LOGN>(lds, mtrunc, tw, need, lio, lio);
 }
 
 // Reconstruct (leopard16.go:432-568) of one stripe, one 32W-byte tile (LTile) per workgroup.
 // F scales rows in and out (full-field tables); FT runs the transforms (F, or
-// F16S when every transform twiddle lies in GF(2^8)).
+// F16S when every transform twiddle lies in GF(2^8)).  The scale-in feeds the
+// IFFT's first pass straight from HBM and the FFT's last pass reveals straight
+// to the output rows.
 template <class F, class FT, int LOGN>
 __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     typedef LTile<F> L;
@@ -1378,25 +1421,38 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     constexpr int N = 1 << LOGN, U = L::U;
     constexpr int K = (N * U + 255) / 256;  // derivative outputs per thread
     __shared__ __attribute__((aligned(16))) uint8_t lds[N * L::ROW];
+    __shared__ int outrow[N];  // work row -> output index (reveal), -1: not revealed
     const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
-    // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0
-    for (int it = threadIdx.x; it < N * U; it += 256) {
-        const int r = it / U, u = it - r * U;
-        V v = F::zero();
-        const uint8_t *src = a.src[r];
-#ifdef RS_REC_ABL_NOSCALE  // ablation (performance experiments only): load without the multiply
-        if (src && L::valid(tile, a.S, u)) v = F::load(src + tile, u);
-#else
-        if (src && L::valid(tile, a.S, u)) F::mul_add(v, F::load(src + tile, u), a.tw_in + (uint64_t)r * F::TWD);
-#endif
-        L::put(lds, r, u, v);
-    }
+    for (int r = threadIdx.x; r < N; r += 256) outrow[r] = -1;
     __syncthreads();
-#ifndef RS_REC_ABL_NOIFFT
-    lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft);
-#endif
+    for (int j = threadIdx.x; j < a.nd; j += 256) outrow[a.pos[j]] = j;  // read after the IFFT's barriers
+    // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0
+    struct ScaleIn {
+        const RecArgs &a;
+        uint64_t tile;
+        __device__ V operator()(int r, int u) const {
+            V v = F::zero();
+            const uint8_t *src = a.src[r];
+            if (src && L::valid(tile, a.S, u)) F::mul_add(v, F::load(src + tile, u), a.tw_in + (uint64_t)r * F::TWD);
+            return v;
+        }
+    };
+    // reveal: shard = work[pos] * (modulus - errLocs[pos])
+    struct Reveal {
+        const RecArgs &a;
+        const int *outrow;
+        uint64_t tile;
+        __device__ void operator()(int r, int u, const V &x) const {
+            const int j = outrow[r];
+            if (j < 0 || !L::valid(tile, a.S, u)) return;
+            V v = F::zero();
+            F::mul_add(v, x, a.tw_out + (uint64_t)j * F::TWD);
+            F::store(a.dst[j] + tile, u, v);
+        }
+    };
+    const LdsIO<FT> lio{lds};
+    lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft, nullptr, ScaleIn{a, tile}, lio);
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
-#ifndef RS_REC_ABL_NODERIV
     {
         V o[K];
 #pragma unroll
@@ -1420,70 +1476,69 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         }
         __syncthreads();
     }
-#endif
-#ifndef RS_REC_ABL_NOFFT
+    const Reveal rv{a, outrow, tile};
     if (a.prune) {
         uint32_t need[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) need[k] = __builtin_amdgcn_readfirstlane(a.need[k]);
-        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, &need);
+        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, &need, lio, rv);
     } else {
-        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft);
-    }
-#endif
-    // reveal: shard = work[pos] * (modulus - errLocs[pos])
-    for (int it = threadIdx.x; it < a.nd * U; it += 256) {
-        const int j = it / U, u = it - j * U;
-        if (!L::valid(tile, a.S, u)) continue;
-        V v = F::zero();
-        F::mul_add(v, L::get(lds, a.pos[j], u), a.tw_out + (uint64_t)j * F::TWD);
-        F::store(a.dst[j] + tile, u, v);
+        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, nullptr, lio, rv);
     }
 }
 
 // Encode for 32 < m <= 256 (leopard16.go:128-224 / leopard8.go:153-277):
-// acc and the current chunk both live in LDS (2 x m rows of the tile).
+// acc and the current chunk both live in LDS (2 x m rows of the tile).  Each
+// chunk's first IFFT pass reads its rows from HBM, its last XORs the results
+// into acc (chunk 0: writes acc), and the FFT's last pass writes the parity
+// rows (or compares them, verify).
 template <class F, int LOGM, bool VERIFY>
 __global__ void __launch_bounds__(256) k_enc_lds(EncodeArgs a) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
-    constexpr int M = 1 << LOGM, U = L::U;
+    constexpr int M = 1 << LOGM;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
     uint8_t *acc = lds_dyn, *cur = lds_dyn + M * L::ROW;
     const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
     const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
     constexpr int its = ifft_slot_count(LOGM);
+    struct ChunkIn {
+        const EncodeArgs &a;
+        int row0, cnt;
+        uint64_t soff, tile;
+        __device__ V operator()(int r, int u) const {
+            if (r < cnt && L::valid(tile, a.shard_size, u)) return F::load(row_ptr(a.data, row0 + r) + soff + tile, u);
+            return F::zero();
+        }
+    };
+    struct AccXor {
+        uint8_t *acc;
+        __device__ void operator()(int r, int u, const V &x) const {
+            V v = L::get(acc, r, u);
+            F::xor_into(v, x);
+            L::put(acc, r, u, v);
+        }
+    };
+    struct ParityOut {
+        const EncodeArgs &a;
+        uint64_t soff, tile;
+        uint32_t *bad;
+        __device__ void operator()(int r, int u, const V &v) const {
+            if (r >= a.p || !L::valid(tile, a.shard_size, u)) return;
+            uint8_t *prow = row_ptr(a.parity, r) + soff + tile;
+            if constexpr (VERIFY) *bad |= F::diff(v, F::load(prow, u));
+            else F::store(prow, u, v);
+        }
+    };
     for (int c = 0; c < a.nchunks; c++) {
         const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
-        uint8_t *dst = c == 0 ? acc : cur;
-        for (int it = threadIdx.x; it < M * U; it += 256) {
-            const int r = it / U, u = it - r * U;
-            V v = F::zero();
-            if (r < cnt && L::valid(tile, a.shard_size, u)) v = F::load(row_ptr(a.data, row0 + r) + soff + tile, u);
-            L::put(dst, r, u, v);
-        }
-        __syncthreads();
-        lds_transform<F, true, LOGM>(dst, cnt, a.tw_ifft + (uint64_t)c * its * F::TWD);
-        if (c > 0) {
-            for (int it = threadIdx.x; it < M * U; it += 256) {
-                const int r = it / U, u = it - r * U;
-                V x = L::get(acc, r, u);
-                F::xor_into(x, L::get(cur, r, u));
-                L::put(acc, r, u, x);
-            }
-            __syncthreads();
-        }
+        const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
+        const ChunkIn in{a, row0, cnt, soff, tile};
+        if (c == 0) lds_transform<F, true, LOGM>(acc, cnt, tw, nullptr, in, LdsIO<F>{acc});
+        else lds_transform<F, true, LOGM>(cur, cnt, tw, nullptr, in, AccXor{acc});
     }
-    lds_transform<F, false, LOGM>(acc, a.p, a.tw_fft);
     uint32_t bad = 0;
-    for (int it = threadIdx.x; it < a.p * U; it += 256) {
-        const int r = it / U, u = it - r * U;
-        if (!L::valid(tile, a.shard_size, u)) continue;
-        uint8_t *prow = row_ptr(a.parity, r) + soff + tile;
-        const V v = L::get(acc, r, u);
-        if constexpr (VERIFY) bad |= F::diff(v, F::load(prow, u));
-        else F::store(prow, u, v);
-    }
+    lds_transform<F, false, LOGM>(acc, a.p, a.tw_fft, nullptr, LdsIO<F>{acc}, ParityOut{a, soff, tile, &bad});
     if constexpr (VERIFY) {
         flag_mismatch(a.mismatch, bad != 0);
     }
