@@ -1257,19 +1257,39 @@ struct LTile {
 };
 
 // Rows [lo, lo + cnt) (cnt a power of two, lo a multiple of cnt) hold a set
-// bit of the 256-bit row mask (wave-uniform words, lane-varying lo).
-__device__ __forceinline__ bool rows_needed(const uint32_t (&w)[8], int lo, int cnt) {
+// bit of the 256-bit row mask (wave-uniform words, lane-varying lo).  Passed
+// by value (Need / NoNeed) so that the words stay in registers: a pointer to
+// a local array through the pass functors left it on the stack (32 B of
+// scratch stores per lane: +67 MB of HBM writes per C4 launch).
+struct Need {
+    uint32_t w[8];
+};
+struct NoNeed {};
+__device__ __forceinline__ bool rows_needed(const Need &n, int lo, int cnt) {
     if (cnt >= 32) {
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < 8; k++)
-            if (k * 32 >= lo && k * 32 < lo + cnt) acc |= w[k];
+            if (k * 32 >= lo && k * 32 < lo + cnt) acc |= n.w[k];
         return acc != 0;
     }
-    uint32_t word = w[0];
+    // a select chain; the opaque step keeps the compiler from turning it into
+    // a lane-indexed load of the words spilled to a stack array
+    const int idx = lo >> 5;
+    uint32_t word = n.w[0];
 #pragma unroll
-    for (int k = 1; k < 8; k++) word = (lo >> 5) == k ? w[k] : word;
+    for (int k = 1; k < 8; k++) {
+        asm volatile("" : "+v"(word));
+        word = idx == k ? n.w[k] : word;
+    }
     return ((word >> (lo & 31)) & ((1u << cnt) - 1)) != 0;
+}
+__device__ __forceinline__ bool rows_needed(const NoNeed &, int, int) { return true; }
+__device__ __forceinline__ Need load_need(const uint32_t (&src)[8]) {
+    Need n;
+#pragma unroll
+    for (int k = 0; k < 8; k++) n.w[k] = __builtin_amdgcn_readfirstlane(src[k]);
+    return n;
 }
 
 // Row sources / sinks of a pass: the LDS image by default; the first pass of
@@ -1301,9 +1321,9 @@ __device__ __forceinline__ void cfor(Fn &&f) {
 // need (forward passes only): skip groups none of whose rows is read later --
 // the pruning of errorBitfield.fftDIT (leopard16.go:1215-1252); the rows that
 // are read come out identical.
-template <class F, bool INV, class In, class Out>
+template <class F, bool INV, class In, class Out, class NeedT>
 __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active, const uint32_t *__restrict__ tw,
-                                         const uint32_t (*need)[8], const In &in, const Out &out) {
+                                         NeedT need, const In &in, const Out &out) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
     constexpr int U = L::U;
@@ -1315,7 +1335,7 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
             const int q = it / U, u = it - q * U;
             const int j = q & (dist - 1);
             const int i = g * 4 * dist + j;
-            if (!INV && need && !rows_needed(*need, g * 4 * dist, 4 * dist)) return;
+            if (!INV && !rows_needed(need, g * 4 * dist, 4 * dist)) return;
             const uint32_t *t = tw + (uint64_t)g * 3 * F::TWD;
             V x0 = in(i, u), x1 = in(i + dist, u), x2 = in(i + 2 * dist, u), x3 = in(i + 3 * dist, u);
             if constexpr (INV) ifft4<F, BF>(x0, x1, x2, x3, t);
@@ -1343,7 +1363,7 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
         for (int it = threadIdx.x; it < pairs * U; it += 256) {
             const int q = it / U, u = it - q * U;
             const int rx = INV ? q : 2 * q, ry = INV ? q + dist : 2 * q + 1;
-            if (!INV && need && !rows_needed(*need, 2 * q, 2)) continue;
+            if (!INV && !rows_needed(need, 2 * q, 2)) continue;
             const uint32_t *t = INV ? tw : tw + (uint64_t)q * F::TWD;
             V x = in(rx, u), y = in(ry, u);
             if constexpr (INV) ifft2<F>(x, y, t);
@@ -1362,12 +1382,12 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
 // first pass reads through `in`, the last writes through `out`.  A first pass
 // that does not read the LDS image runs every group (rows past mtrunc come in
 // as zero, and zero rows transform to zero rows): later passes read those rows.
-template <class F, bool INV, int LOGN, class In, class Out>
+template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed>
 __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
-                                              const uint32_t (*need)[8], const In &in, const Out &out) {
+                                              NeedT need, const In &in, const Out &out) {
     constexpr int N = 1 << LOGN, NP4 = LOGN / 2, NP = NP4 + (LOGN & 1);
     const LdsIO<F> lio{lds};
-    cfor<NP>([&](auto PI) {
+    cfor<NP>([=](auto PI) {  // by value: a captured reference to `need` kept it on the stack
         constexpr int p = decltype(PI)::value;
         constexpr bool radix4 = p < NP4;
         // IFFT: radix-4 passes at dist 4^p (groups N / (4 dist)), then radix-2 at dist N/2;
@@ -1387,8 +1407,9 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
             active = INV ? 1 : (mtrunc + 1) / 2 < N / 2 ? (mtrunc + 1) / 2 : N / 2;
         }
         const uint32_t *t = tw + (uint64_t)slot * F::TWD;
-        auto run = [&](const auto &pin, const auto &pout) {
-            lds_pass<F, INV>(dist, radix4 ? 4 : 2, active, t, INV ? nullptr : need, pin, pout);
+        auto run = [=](const auto &pin, const auto &pout) {
+            if constexpr (INV) lds_pass<F, INV>(dist, radix4 ? 4 : 2, active, t, NoNeed{}, pin, pout);
+            else lds_pass<F, INV>(dist, radix4 ? 4 : 2, active, t, need, pin, pout);
         };
         if constexpr (p == 0 && !IsLdsIO<In>::value) {
             if constexpr (radix4) active = groups;
@@ -1403,10 +1424,9 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
     });
 }
 template <class F, bool INV, int LOGN>
-__device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
-                                              const uint32_t (*need)[8] = nullptr) {
+__device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw) {
     const LdsIO<F> lio{lds};
-    lds_transform<F, INV, LOGN>(lds, mtrunc, tw, need, lio, lio);
+    lds_transform<F, INV, LOGN>(lds, mtrunc, tw, NoNeed{}, lio, lio);
 }
 
 // Reconstruct (leopard16.go:432-568) of one stripe, one 32W-byte tile (LTile) per workgroup.
@@ -1451,7 +1471,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         }
     };
     const LdsIO<FT> lio{lds};
-    lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft, nullptr, ScaleIn{a, tile}, lio);
+    lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile}, lio);
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
     {
         V o[K];
@@ -1478,12 +1498,9 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     }
     const Reveal rv{a, outrow, tile};
     if (a.prune) {
-        uint32_t need[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) need[k] = __builtin_amdgcn_readfirstlane(a.need[k]);
-        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, &need, lio, rv);
+        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, load_need(a.need), lio, rv);
     } else {
-        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, nullptr, lio, rv);
+        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
     }
 }
 
@@ -1534,11 +1551,11 @@ __global__ void __launch_bounds__(256) k_enc_lds(EncodeArgs a) {
         const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
         const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
         const ChunkIn in{a, row0, cnt, soff, tile};
-        if (c == 0) lds_transform<F, true, LOGM>(acc, cnt, tw, nullptr, in, LdsIO<F>{acc});
-        else lds_transform<F, true, LOGM>(cur, cnt, tw, nullptr, in, AccXor{acc});
+        if (c == 0) lds_transform<F, true, LOGM>(acc, cnt, tw, NoNeed{}, in, LdsIO<F>{acc});
+        else lds_transform<F, true, LOGM>(cur, cnt, tw, NoNeed{}, in, AccXor{acc});
     }
     uint32_t bad = 0;
-    lds_transform<F, false, LOGM>(acc, a.p, a.tw_fft, nullptr, LdsIO<F>{acc}, ParityOut{a, soff, tile, &bad});
+    lds_transform<F, false, LOGM>(acc, a.p, a.tw_fft, NoNeed{}, LdsIO<F>{acc}, ParityOut{a, soff, tile, &bad});
     if constexpr (VERIFY) {
         flag_mismatch(a.mismatch, bad != 0);
     }
@@ -1694,10 +1711,7 @@ __global__ void __launch_bounds__(256, 2) k_rec_r16(RecArgs a) {
     // and reveal: shard = work[pos] * (modulus - errLocs[pos])
     bool live = 16 * G < a.mtrunc;
     if (live && a.prune) {
-        uint32_t need[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) need[k] = __builtin_amdgcn_readfirstlane(a.need[k]);
-        live = rows_needed(need, 16 * G, 16);
+        live = rows_needed(load_need(a.need), 16 * G, 16);
     }
     if (live) {
 #pragma unroll
