@@ -1399,21 +1399,20 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
             for (int q = 0; q < p; q++) sl += 3 * (INV ? N / (4 << (2 * q)) : (1 << (2 * q)));
             return sl;
         }();
+        constexpr bool from_hbm = p == 0 && !IsLdsIO<In>::value;  // every group (see above)
         int active;
         if constexpr (radix4) {
             active = (mtrunc + 4 * dist - 1) / (4 * dist);
-            if (active > groups) active = groups;
+            if (active > groups || from_hbm) active = groups;
         } else {
-            active = INV ? 1 : (mtrunc + 1) / 2 < N / 2 ? (mtrunc + 1) / 2 : N / 2;
+            active = INV ? 1 : (mtrunc + 1) / 2 < N / 2 && !from_hbm ? (mtrunc + 1) / 2 : N / 2;
         }
         const uint32_t *t = tw + (uint64_t)slot * F::TWD;
         auto run = [=](const auto &pin, const auto &pout) {
             if constexpr (INV) lds_pass<F, INV>(dist, radix4 ? 4 : 2, active, t, NoNeed{}, pin, pout);
             else lds_pass<F, INV>(dist, radix4 ? 4 : 2, active, t, need, pin, pout);
         };
-        if constexpr (p == 0 && !IsLdsIO<In>::value) {
-            if constexpr (radix4) active = groups;
-            else active = INV ? 1 : N / 2;
+        if constexpr (from_hbm) {
             if constexpr (p == NP - 1) run(in, out);
             else run(in, lio);
         } else if constexpr (p == NP - 1) {
