@@ -15,6 +15,7 @@
 #include <cstring>
 #include <list>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -83,6 +84,25 @@ struct RecPlan {
     std::vector<uint32_t> tw_in, tw_out;
 };
 
+// A cached reconstruct plan with its per-pattern tables (scale-in / reveal
+// images, rebuilt-row positions) resident in HBM: rs_reconstruct_dev of a
+// pattern seen before uploads only its row pointers.
+struct DevPlan {
+    RecPlan pl;
+    DevBuf<uint8_t> blob;
+    const uint32_t *tw_in = nullptr, *tw_out = nullptr;
+    const int *pos = nullptr;
+    uint32_t need[8] = {};
+    hipEvent_t used = nullptr;  // recorded after every launch that reads blob
+    ~DevPlan() {
+        if (used) {
+            (void)hipEventSynchronize(used);
+            (void)hipEventDestroy(used);
+        }
+        blob.release();
+    }
+};
+
 }  // namespace
 
 struct rs_codec {
@@ -132,6 +152,17 @@ struct rs_codec {
 
     // reconstruct plans keyed by (erasure pattern, recover_all) (bounded LRU)
     std::list<std::pair<std::vector<uint8_t>, RecPlan>> plan_cache;
+    // device-resident plans of rs_reconstruct_dev (same key), and a ring of
+    // per-call row-pointer slots (pinned host + HBM), each reusable once the
+    // launch that read it has finished (ring_ev)
+    std::list<std::pair<std::vector<uint8_t>, std::unique_ptr<DevPlan>>> dplan_cache;
+    static constexpr int kRing = 8;
+    DevBuf<uint8_t> ring_dev;
+    uint8_t *ring_host = nullptr;
+    size_t ring_slot = 0;  // bytes per slot
+    hipEvent_t ring_ev[kRing] = {};
+    bool ring_used[kRing] = {};
+    int ring_next = 0;
 
     // error-locator cache keyed by erasure pattern (bounded LRU)
     std::list<std::pair<std::vector<uint8_t>, std::vector<uint32_t>>> el_cache;
@@ -167,6 +198,14 @@ struct rs_codec {
         if (dflag) (void)hipFree(dflag);
         rc_blob.release();
         if (rc_host) (void)hipHostFree(rc_host);
+        dplan_cache.clear();  // each plan waits for its last launch
+        for (int i = 0; i < kRing; i++)
+            if (ring_ev[i]) {
+                (void)hipEventSynchronize(ring_ev[i]);
+                (void)hipEventDestroy(ring_ev[i]);
+            }
+        ring_dev.release();
+        if (ring_host) (void)hipHostFree(ring_host);
         if (s_in) (void)hipStreamSynchronize(s_in);
         if (s_out) (void)hipStreamSynchronize(s_out);
         stage.release();
@@ -645,6 +684,92 @@ int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipS
     e = run_passes(c, false, w, S, c->logn, c->m + c->k, c->dtw_fft.p, s);
     if (e) return e;
     if (nd) HIP_TRY(launch_reveal(c->bits, c->rc_dst + (size_t)set * nd, w, S, c->rc_pos, c->rc_tw_out, nd, s));
+    return RS_OK;
+}
+
+// Device-resident plan for (present, recover_all), built and uploaded on first use.
+int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, DevPlan **out) {
+    std::vector<uint8_t> key(present);
+    key.push_back(recover_all ? 1 : 0);
+    for (auto it = c->dplan_cache.begin(); it != c->dplan_cache.end(); ++it) {
+        if (it->first == key) {
+            c->dplan_cache.splice(c->dplan_cache.begin(), c->dplan_cache, it);
+            *out = c->dplan_cache.front().second.get();
+            return RS_OK;
+        }
+    }
+    auto dp = std::make_unique<DevPlan>();
+    if (int e = plan_reconstruct(c, present, recover_all, dp->pl)) return e;
+    const RecPlan &pl = dp->pl;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t s_in = pl.tw_in.size() * 4, s_out = pl.tw_out.size() * 4, s_pos = std::max<size_t>(pl.pos.size(), 1) * 4;
+    const size_t o_out = al(s_in), o_pos = o_out + al(s_out), total = o_pos + al(s_pos);
+    std::vector<uint8_t> h(total, 0);
+    std::memcpy(h.data(), pl.tw_in.data(), s_in);
+    std::memcpy(h.data() + o_out, pl.tw_out.data(), s_out);
+    if (!pl.pos.empty()) std::memcpy(h.data() + o_pos, pl.pos.data(), pl.pos.size() * 4);
+    HIP_TRY(dp->blob.ensure(total));
+    HIP_TRY(hipMemcpy(dp->blob.p, h.data(), total, hipMemcpyHostToDevice));
+    dp->tw_in = (const uint32_t *)dp->blob.p;
+    dp->tw_out = (const uint32_t *)(dp->blob.p + o_out);
+    dp->pos = (const int *)(dp->blob.p + o_pos);
+    for (int p : pl.pos) dp->need[p >> 5] |= 1u << (p & 31);
+    HIP_TRY(hipEventCreateWithFlags(&dp->used, hipEventDisableTiming));
+    c->dplan_cache.emplace_front(std::move(key), std::move(dp));
+    if (c->dplan_cache.size() > 16) c->dplan_cache.pop_back();  // waits for the plan's last launch
+    *out = c->dplan_cache.front().second.get();
+    return RS_OK;
+}
+
+// rs_reconstruct_dev with n <= 256 (one LDS-resident launch): the plan's tables
+// stay in HBM, the row pointers go through a ring slot, and nothing waits for
+// the kernel -- the call is stream-ordered like the device encodes.
+int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uint8_t> &present, uint64_t S,
+                           bool recover_all, hipStream_t s) {
+    DevPlan *dp = nullptr;
+    if (int e = dev_plan(c, present, recover_all, &dp)) return e;
+    const RecPlan &pl = dp->pl;
+    const int n = c->n, nd = (int)pl.dst_shard.size();
+    if (!nd) return RS_OK;
+    const size_t bytes = ((size_t)(n + nd) * sizeof(void *) + 255) & ~(size_t)255;
+    if (c->ring_slot < bytes) {
+        for (int i = 0; i < rs_codec::kRing; i++)
+            if (c->ring_used[i]) HIP_TRY(hipEventSynchronize(c->ring_ev[i]));
+        if (c->ring_host) HIP_TRY(hipHostFree(c->ring_host));
+        c->ring_host = nullptr;
+        c->ring_slot = 0;
+        HIP_TRY(c->ring_dev.ensure(bytes * rs_codec::kRing));
+        HIP_TRY(hipHostMalloc((void **)&c->ring_host, bytes * rs_codec::kRing, hipHostMallocDefault));
+        c->ring_slot = bytes;
+    }
+    const int i = c->ring_next;
+    c->ring_next = (i + 1) % rs_codec::kRing;
+    if (!c->ring_ev[i]) HIP_TRY(hipEventCreateWithFlags(&c->ring_ev[i], hipEventDisableTiming));
+    if (c->ring_used[i]) HIP_TRY(hipEventSynchronize(c->ring_ev[i]));  // its copy and kernel are done
+    uint8_t *h = c->ring_host + (size_t)i * c->ring_slot;
+    uint8_t *g = c->ring_dev.p + (size_t)i * c->ring_slot;
+    const uint8_t **src = (const uint8_t **)h;
+    uint8_t **dst = (uint8_t **)h + n;
+    for (int r = 0; r < n; r++) src[r] = pl.src_shard[r] >= 0 ? d[pl.src_shard[r]] : nullptr;
+    for (int j = 0; j < nd; j++) dst[j] = d[pl.dst_shard[j]];
+    HIP_TRY(hipMemcpyAsync(g, h, (size_t)(n + nd) * sizeof(void *), hipMemcpyHostToDevice, s));
+    RecArgs ra{};
+    ra.src = (const uint8_t *const *)g;
+    ra.dst = (uint8_t *const *)g + n;
+    ra.pos = dp->pos;
+    ra.tw_in = dp->tw_in;
+    ra.tw_out = dp->tw_out;
+    ra.tw_ifft = c->dtw_ifft.p;
+    ra.tw_fft = c->dtw_fft.p;
+    ra.S = S;
+    ra.mtrunc = c->m + c->k;
+    ra.nd = nd;
+    ra.prune = prune_enabled() ? 1 : 0;
+    std::memcpy(ra.need, dp->need, sizeof(ra.need));
+    HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
+    HIP_TRY(hipEventRecord(c->ring_ev[i], s));
+    c->ring_used[i] = true;
+    HIP_TRY(hipEventRecord(dp->used, s));
     return RS_OK;
 }
 
@@ -1219,7 +1344,14 @@ int rs_reconstruct_dev(rs_codec *c, uint8_t *const *d, const uint8_t *present, s
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (int ie = ensure_device(c)) return ie;
-    return reconstruct_device(c, d, pr, S, recover_all != 0, pick_stream(c, stream));
+    const hipStream_t s = pick_stream(c, stream);
+    if (int e = build_decode_plan(c)) return e;
+    if (c->dec_ok && c->logn <= kMaxLdsLogN) {
+        if (int e = reconstruct_device_lds(c, d, pr, S, recover_all != 0, s)) return e;
+        if (!stream) HIP_TRY(hipStreamSynchronize(s));  // no caller stream: complete on return
+        return RS_OK;
+    }
+    return reconstruct_device(c, d, pr, S, recover_all != 0, s);
 }
 
 int rs_encode(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshards) {

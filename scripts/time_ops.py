@@ -126,13 +126,15 @@ def main():
         present = np.ones(k + p, bool)
         present[np.random.default_rng(0x5EED).choice(k + p, ne, replace=False)] = False
 
-        def run():
+        st = torch.cuda.current_stream()
+
+        def run():  # stream-ordered on the timing stream (verify reads its flag back)
             if op == "encode":
-                c.encode_dev_batch(slab)
+                c.encode_dev_batch(slab, st)
             elif op == "verify":
-                c.verify_dev(rows)
+                c.verify_dev(rows, st)
             else:
-                c.reconstruct_dev(rows, present)
+                c.reconstruct_dev(rows, present, stream=st)
 
         for _ in range(5):
             run()

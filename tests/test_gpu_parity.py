@@ -655,3 +655,35 @@ def test_radix16_encode_verify(torch_dev, monkeypatch, r16, k, p, S):
     assert c.verify_dev(one)
     one[k + p - 1, S - 1] ^= 1
     assert not c.verify_dev(one)
+
+
+def test_reconstruct_dev_async_ring_and_plan_eviction(torch_dev):
+    """rs_reconstruct_dev on a caller stream returns without waiting: 40 calls
+    back to back over 20 erasure patterns (more than the 8 row-pointer ring
+    slots and the 16 cached device plans, so slots are reused and plans
+    evicted while launches are in flight), each on its own copy of the stripe,
+    all checked after one synchronize."""
+    torch = torch_dev
+    k, p, S = 128, 32, 4096
+    g = torch.Generator(device="cuda")
+    g.manual_seed(21)
+    full = torch.randint(0, 256, (k + p, S), dtype=torch.uint8, device="cuda", generator=g)
+    c = rs.New16(k, p)
+    c.encode_dev(full)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(21)
+    pats = [rng.choice(k + p, int(rng.integers(1, p + 1)), replace=False) for _ in range(20)]
+    st = torch.cuda.Stream()
+    copies = []
+    with torch.cuda.stream(st):
+        for i in range(40):
+            er = pats[i % 20]
+            present = np.ones(k + p, bool)
+            present[er] = False
+            t = full.clone()
+            t[torch.from_numpy(er).cuda()] = 0
+            c.reconstruct_dev(t, present, stream=st)
+            copies.append(t)
+    st.synchronize()
+    for i, t in enumerate(copies):
+        assert torch.equal(t, full), f"call {i}"
