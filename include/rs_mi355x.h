@@ -137,10 +137,16 @@ int rs_host_register(void *ptr, size_t bytes);
 int rs_host_unregister(void *ptr);
 
 /* ---------------- Device-resident entry points (HBM in, HBM out) ---------------- */
+/* Streams: a hipStream_t (asynchronous on it), NULL (the codec's own stream;
+ * the call completes before it returns), or RS_NULL_STREAM: HIP's null
+ * (legacy default) stream, asynchronous -- the handle 0 a caller's default
+ * stream has (torch.cuda.default_stream().cuda_stream == 0), which NULL
+ * cannot express. */
+#define RS_NULL_STREAM ((void *)~(uintptr_t)0)
 /* d_shards: HOST array of k+p DEVICE pointers, each to shard_size bytes
- * (4-byte aligned; 64-byte aligned recommended).  stream: hipStream_t or NULL
- * for the codec's own stream.  rs_encode_dev is asynchronous on `stream` when
- * the rows are equally strided (the common AllocAligned slab layout); the
+ * (4-byte aligned; 64-byte aligned recommended).  rs_encode_dev is
+ * asynchronous on a caller stream when the rows are equally strided (the
+ * common AllocAligned slab layout), rs_reconstruct_dev when n <= 256; the
  * other calls return after their work is complete. */
 int rs_encode_dev(rs_codec *codec, uint8_t *const *d_shards, size_t shard_size, void *stream);
 int rs_verify_dev(rs_codec *codec, uint8_t *const *d_shards, size_t shard_size, int *ok, void *stream);

@@ -144,12 +144,20 @@ def _dev_rows(rows, total: int):
     return ptrs, S or 0
 
 
+RS_NULL_STREAM = C.c_void_p(-1).value  # include/rs_mi355x.h: HIP's null stream, asynchronous
+
+
 def _stream_handle(stream):
+    """torch stream (default: the current one) -> the C-ABI stream argument.
+    torch's default stream has handle 0, which the C-ABI reads as "the codec's
+    own stream, synchronous": pass it as RS_NULL_STREAM so calls on it stay
+    asynchronous and ordered with torch's work."""
     if stream is None:
         import torch
 
-        return torch.cuda.current_stream().cuda_stream
-    return getattr(stream, "cuda_stream", stream)
+        stream = torch.cuda.current_stream()
+    h = getattr(stream, "cuda_stream", stream)
+    return RS_NULL_STREAM if h in (0, None) and stream is not None and hasattr(stream, "cuda_stream") else h
 
 
 # --------------------------------------------------------------------------- codec

@@ -137,6 +137,7 @@ struct rs_codec {
     // host-side overwrite or a reallocation).
     hipEvent_t scratch_ev = nullptr;
     bool scratch_used = false;
+    hipStream_t scratch_stream = nullptr;  // stream of the last scratch user
     DevBuf<uint8_t> work;
     DevBuf<uint8_t *> rows;         // row-pointer table (non-strided inputs)
     std::vector<uint8_t *> rows_host;
@@ -368,11 +369,21 @@ int build_decode_plan(rs_codec *c) {
     return upload_twiddles(c, fl, c->dtw_fft);
 }
 
-hipStream_t pick_stream(rs_codec *c, void *s) { return s ? (hipStream_t)s : c->stream; }
+hipStream_t pick_stream(rs_codec *c, void *s) {
+    return s == RS_NULL_STREAM ? (hipStream_t)0 : s ? (hipStream_t)s : c->stream;
+}
 
-// Order this call's stream behind the previous user of the codec scratch.
+// Order this call's stream behind the previous user of the codec scratch
+// (nothing to do when that was this stream: it is in order already, and an
+// explicit wait would stop the next launch from being queued behind the
+// previous one).
+bool scratch_wait_same_stream() {
+    const char *e = getenv("RS_SCRATCH_SAME_STREAM");  // "wait": A/B experiments only
+    return e && e[0] == 'w';
+}
 int scratch_acquire(rs_codec *c, hipStream_t s) {
-    if (c->scratch_used) HIP_TRY(hipStreamWaitEvent(s, c->scratch_ev, 0));
+    if (c->scratch_used && (s != c->scratch_stream || scratch_wait_same_stream()))
+        HIP_TRY(hipStreamWaitEvent(s, c->scratch_ev, 0));
     return RS_OK;
 }
 // Host wait for the previous user of the scratch (before a host-side write or a reallocation).
@@ -385,6 +396,7 @@ int scratch_release(rs_codec *c, hipStream_t s) {
     if (!c->scratch_ev) HIP_TRY(hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(c->scratch_ev, s));
     c->scratch_used = true;
+    c->scratch_stream = s;
     return RS_OK;
 }
 // DevBuf::ensure for codec scratch: a reallocation frees a buffer that a

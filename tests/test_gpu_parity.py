@@ -687,3 +687,28 @@ def test_reconstruct_dev_async_ring_and_plan_eviction(torch_dev):
     st.synchronize()
     for i, t in enumerate(copies):
         assert torch.equal(t, full), f"call {i}"
+
+
+def test_default_stream_is_stream_ordered(torch_dev):
+    """torch's default stream (handle 0) goes to the C-ABI as RS_NULL_STREAM:
+    the calls are asynchronous on it and ordered with torch's own work there
+    (no synchronize between the encode / reconstruct and the reads)."""
+    torch = torch_dev
+    k, p, S = 128, 32, 1 << 16
+    c = rs.New16(k, p)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    slab = torch.randint(0, 256, (k + p, S), dtype=torch.uint8, device="cuda", generator=g)
+    ref = slab.clone()
+    c.encode_dev(ref)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        t = slab.clone()
+        c.encode_dev(t)  # default stream
+        par = t[k:].clone()  # torch kernel on the same stream, after the encode
+        er = torch.tensor([0, 5, k + 1])
+        t[er] = 0
+        present = np.ones(k + p, bool)
+        present[er.numpy()] = False
+        c.reconstruct_dev(t, present)
+        assert torch.equal(par, ref[k:]) and torch.equal(t, ref)
