@@ -92,6 +92,7 @@ struct DevPlan {
     DevBuf<uint8_t> blob;
     const uint32_t *tw_in = nullptr, *tw_out = nullptr;
     const int *pos = nullptr;
+    const int *src_idx = nullptr, *dst_idx = nullptr;  // pl.src_shard / pl.dst_shard (strided launches)
     uint32_t need[8] = {};
     hipEvent_t used = nullptr;  // recorded after every launch that reads blob
     ~DevPlan() {
@@ -715,16 +716,22 @@ int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
     const RecPlan &pl = dp->pl;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t s_in = pl.tw_in.size() * 4, s_out = pl.tw_out.size() * 4, s_pos = std::max<size_t>(pl.pos.size(), 1) * 4;
-    const size_t o_out = al(s_in), o_pos = o_out + al(s_out), total = o_pos + al(s_pos);
+    const size_t s_si = pl.src_shard.size() * 4, s_di = std::max<size_t>(pl.dst_shard.size(), 1) * 4;
+    const size_t o_out = al(s_in), o_pos = o_out + al(s_out), o_si = o_pos + al(s_pos), o_di = o_si + al(s_si);
+    const size_t total = o_di + al(s_di);
     std::vector<uint8_t> h(total, 0);
     std::memcpy(h.data(), pl.tw_in.data(), s_in);
     std::memcpy(h.data() + o_out, pl.tw_out.data(), s_out);
     if (!pl.pos.empty()) std::memcpy(h.data() + o_pos, pl.pos.data(), pl.pos.size() * 4);
+    std::memcpy(h.data() + o_si, pl.src_shard.data(), s_si);
+    if (!pl.dst_shard.empty()) std::memcpy(h.data() + o_di, pl.dst_shard.data(), pl.dst_shard.size() * 4);
     HIP_TRY(dp->blob.ensure(total));
     HIP_TRY(hipMemcpy(dp->blob.p, h.data(), total, hipMemcpyHostToDevice));
     dp->tw_in = (const uint32_t *)dp->blob.p;
     dp->tw_out = (const uint32_t *)(dp->blob.p + o_out);
     dp->pos = (const int *)(dp->blob.p + o_pos);
+    dp->src_idx = (const int *)(dp->blob.p + o_si);
+    dp->dst_idx = (const int *)(dp->blob.p + o_di);
     for (int p : pl.pos) dp->need[p >> 5] |= 1u << (p & 31);
     HIP_TRY(hipEventCreateWithFlags(&dp->used, hipEventDisableTiming));
     c->dplan_cache.emplace_front(std::move(key), std::move(dp));
@@ -734,8 +741,10 @@ int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
 }
 
 // rs_reconstruct_dev with n <= 256 (one LDS-resident launch): the plan's tables
-// stay in HBM, the row pointers go through a ring slot, and nothing waits for
-// the kernel -- the call is stream-ordered like the device encodes.
+// stay in HBM; equally strided shards (an AllocAligned slab, a torch 2-D
+// tensor) go to the kernel as base + stride, other layouts' row pointers
+// through a ring slot; nothing waits for the kernel -- the call is
+// stream-ordered like the device encodes.
 int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uint8_t> &present, uint64_t S,
                            bool recover_all, hipStream_t s) {
     DevPlan *dp = nullptr;
@@ -743,6 +752,42 @@ int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uin
     const RecPlan &pl = dp->pl;
     const int n = c->n, nd = (int)pl.dst_shard.size();
     if (!nd) return RS_OK;
+    RecArgs ra{};
+    ra.pos = dp->pos;
+    ra.tw_in = dp->tw_in;
+    ra.tw_out = dp->tw_out;
+    ra.tw_ifft = c->dtw_ifft.p;
+    ra.tw_fft = c->dtw_fft.p;
+    ra.S = S;
+    ra.mtrunc = c->m + c->k;
+    ra.nd = nd;
+    ra.prune = prune_enabled() ? 1 : 0;
+    std::memcpy(ra.need, dp->need, sizeof(ra.need));
+    {
+        // strided: every shard the launch touches at d[0] + i * stride
+        int i0 = -1, i1 = -1;
+        for (int i = 0; i < c->total && i1 < 0; i++)
+            if (d[i]) (i0 < 0 ? i0 : i1) = i;
+        bool strided = i0 >= 0 && i1 >= 0 && d[i1] > d[i0] && (uint64_t)(d[i1] - d[i0]) % (uint64_t)(i1 - i0) == 0;
+        const uint64_t stride = strided ? (uint64_t)(d[i1] - d[i0]) / (uint64_t)(i1 - i0) : 0;
+        uint8_t *base = strided ? d[i0] - (uint64_t)i0 * stride : nullptr;
+        strided = strided && stride >= S;
+        for (int i = 0; i < c->total && strided; i++)
+            if (d[i] && d[i] != base + (uint64_t)i * stride) strided = false;
+        for (int r = 0; r < n && strided; r++)
+            if (pl.src_shard[r] >= 0 && !d[pl.src_shard[r]]) strided = false;
+        for (int j = 0; j < nd && strided; j++)
+            if (!d[pl.dst_shard[j]]) strided = false;
+        if (strided) {
+            ra.base = base;
+            ra.stride = stride;
+            ra.src_idx = dp->src_idx;
+            ra.dst_idx = dp->dst_idx;
+            HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
+            HIP_TRY(hipEventRecord(dp->used, s));
+            return RS_OK;
+        }
+    }
     const size_t bytes = ((size_t)(n + nd) * sizeof(void *) + 255) & ~(size_t)255;
     if (c->ring_slot < bytes) {
         for (int i = 0; i < rs_codec::kRing; i++)
@@ -765,19 +810,8 @@ int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uin
     for (int r = 0; r < n; r++) src[r] = pl.src_shard[r] >= 0 ? d[pl.src_shard[r]] : nullptr;
     for (int j = 0; j < nd; j++) dst[j] = d[pl.dst_shard[j]];
     HIP_TRY(hipMemcpyAsync(g, h, (size_t)(n + nd) * sizeof(void *), hipMemcpyHostToDevice, s));
-    RecArgs ra{};
     ra.src = (const uint8_t *const *)g;
     ra.dst = (uint8_t *const *)g + n;
-    ra.pos = dp->pos;
-    ra.tw_in = dp->tw_in;
-    ra.tw_out = dp->tw_out;
-    ra.tw_ifft = c->dtw_ifft.p;
-    ra.tw_fft = c->dtw_fft.p;
-    ra.S = S;
-    ra.mtrunc = c->m + c->k;
-    ra.nd = nd;
-    ra.prune = prune_enabled() ? 1 : 0;
-    std::memcpy(ra.need, dp->need, sizeof(ra.need));
     HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
     HIP_TRY(hipEventRecord(c->ring_ev[i], s));
     c->ring_used[i] = true;

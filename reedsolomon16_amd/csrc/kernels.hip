@@ -1451,7 +1451,13 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         uint64_t tile;
         __device__ V operator()(int r, int u) const {
             V v = F::zero();
-            const uint8_t *src = a.src[r];
+            const uint8_t *src;
+            if (a.base) {
+                const int i = a.src_idx[r];
+                src = i >= 0 ? a.base + (uint64_t)i * a.stride : nullptr;
+            } else {
+                src = a.src[r];
+            }
             if (src && L::valid(tile, a.S, u)) F::mul_add(v, F::load(src + tile, u), a.tw_in + (uint64_t)r * F::TWD);
             return v;
         }
@@ -1466,7 +1472,8 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
             if (j < 0 || !L::valid(tile, a.S, u)) return;
             V v = F::zero();
             F::mul_add(v, x, a.tw_out + (uint64_t)j * F::TWD);
-            F::store(a.dst[j] + tile, u, v);
+            uint8_t *dst = a.base ? a.base + (uint64_t)a.dst_idx[j] * a.stride : a.dst[j];
+            F::store(dst + tile, u, v);
         }
     };
     const LdsIO<FT> lio{lds};
@@ -2013,7 +2020,7 @@ hipError_t rec_lds_w(int bits, int logn, bool sub, const RecArgs &a, hipStream_t
     return sub ? rec_lds_f<F16<W>, F16S<W>>(logn, a, s) : rec_lds_f<F16<W>>(logn, a, s);
 }
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s) {
-    if (bits == 16 && logn == 8 && r16_pick((a.S + R16::TB - 1) / R16::TB)) {
+    if (bits == 16 && logn == 8 && !a.base && r16_pick((a.S + R16::TB - 1) / R16::TB)) {
         const dim3 grid((unsigned)((a.S + R16::TB - 1) / R16::TB));
         if (sub) hipLaunchKernelGGL((k_rec_r16<F16S<2>>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_rec_r16<F16<2>>), grid, dim3(256), 0, s, a);

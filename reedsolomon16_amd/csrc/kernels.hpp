@@ -68,6 +68,12 @@ hipError_t launch_reveal(int bits, uint8_t *const *dst, const uint8_t *work, uin
 struct RecArgs {
     const uint8_t *const *src;  // n device row pointers (nullptr: zero row)
     uint8_t *const *dst;        // nd output rows
+    // strided shards (base != nullptr, LDS-resident kernel only): shard i at
+    // base + i*stride; work row r reads shard src_idx[r] (-1: zero row),
+    // output j is shard dst_idx[j]; src / dst are then unused
+    uint8_t *base;
+    uint64_t stride;
+    const int *src_idx, *dst_idx;
     const int *pos;             // work row of each output
     const uint32_t *tw_in;      // n tables: errLocs scalings (mulgf16 semantics)
     const uint32_t *tw_out;     // nd tables: modulus - errLocs[pos]

@@ -712,3 +712,33 @@ def test_default_stream_is_stream_ordered(torch_dev):
         present[er.numpy()] = False
         c.reconstruct_dev(t, present)
         assert torch.equal(par, ref[k:]) and torch.equal(t, ref)
+
+
+def test_reconstruct_dev_async_row_lists(torch_dev):
+    """The pointer-ring path of rs_reconstruct_dev: shards as separately
+    allocated rows (not equally strided), 24 calls over 12 patterns on a caller
+    stream, checked after one synchronize."""
+    torch = torch_dev
+    k, p, S = 128, 32, 2048
+    g = torch.Generator(device="cuda")
+    g.manual_seed(22)
+    full = torch.randint(0, 256, (k + p, S), dtype=torch.uint8, device="cuda", generator=g)
+    c = rs.New16(k, p)
+    c.encode_dev(full)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(22)
+    pats = [rng.choice(k + p, int(rng.integers(1, p + 1)), replace=False) for _ in range(12)]
+    st = torch.cuda.Stream()
+    calls = []
+    with torch.cuda.stream(st):
+        for i in range(24):
+            er = pats[i % 12]
+            present = np.ones(k + p, bool)
+            present[er] = False
+            rows = [full[r].clone() if present[r] else torch.zeros(S, dtype=torch.uint8, device="cuda")
+                    for r in range(k + p)]
+            c.reconstruct_dev(rows, present, stream=st)
+            calls.append(rows)
+    st.synchronize()
+    for i, rows in enumerate(calls):
+        assert torch.equal(torch.stack(rows), full), f"call {i}"
