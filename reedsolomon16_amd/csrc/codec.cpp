@@ -682,6 +682,8 @@ int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipS
         ra.tw_fft = c->dtw_fft.p;
         ra.S = S;
         ra.mtrunc = c->m + c->k;
+    ra.m = c->m;
+        ra.m = c->m;
         ra.nd = nd;
         ra.prune = prune_enabled() ? 1 : 0;
         for (int p : pl.pos) ra.need[p >> 5] |= 1u << (p & 31);
@@ -760,6 +762,7 @@ int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uin
     ra.tw_fft = c->dtw_fft.p;
     ra.S = S;
     ra.mtrunc = c->m + c->k;
+    ra.m = c->m;
     ra.nd = nd;
     ra.prune = prune_enabled() ? 1 : 0;
     std::memcpy(ra.need, dp->need, sizeof(ra.need));

@@ -1193,6 +1193,15 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 // tile must cover whole 64-byte blocks (low bytes [0,32), high bytes
 // [32,64)), so W = 1 (32-byte tiles) is invalid: the parity tests reject it.
 constexpr uint64_t kLdsMinGrid = 512;
+#ifndef RS_REC_LDS_OUTROW
+#define RS_REC_LDS_OUTROW 0  // 1: reveal through an LDS row -> output table (1 KB more LDS per workgroup)
+#endif
+#ifndef RS_REC_NO_ZSKIP
+#define RS_REC_NO_ZSKIP 0  // 1: the from-HBM IFFT pass transforms the all-zero groups past mtrunc too (A/B)
+#endif
+#ifndef RS_REC_UNFUSED_DERIV
+#define RS_REC_UNFUSED_DERIV 0  // 1: formal derivative as its own LDS pass (A/B experiments)
+#endif
 #ifndef RS_LDS_BRANCHFREE
 #define RS_LDS_BRANCHFREE 1
 #endif
@@ -1214,29 +1223,48 @@ bool pick_narrow(bool automatic) {
     return o < 0 ? automatic : o == 1;
 }
 
+#ifndef RS_LDS_SWZ
+#define RS_LDS_SWZ 0  // 1: swizzled unpadded LDS rows for 128-byte GF(2^16) tiles (measured slower)
+#endif
 template <class F>
 struct LTile {
     static_assert(!F::SYM16 || F::W >= 2, "a GF(2^16) LDS tile must cover whole 64-byte blocks (W >= 2)");
     static constexpr bool W16 = F::SYM16;
     static constexpr int TB = 32 * F::W;                  // bytes of each row owned by a workgroup
-    static constexpr int ROW = TB + RS_LDS_PAD;           // LDS row stride (TB + 16 = 144 B at TB = 128)
+    // 128-byte GF(2^16) tiles: rows of exactly 128 B, [lo of units 0..3][hi of
+    // units 0..3], with address bits 4-7 XORed by a GF(2)-linear function of
+    // row bits 0-4 (bit 7 only from row bits >= 1, so the map is a bijection).
+    // Under the ds_read_b128 / ds_write_b128 lane groups of MI355X_MICROARCH.md
+    // §LDS, every pass of k_rec_lds / k_enc_lds (4 lanes per row, rows 1 or 4
+    // apart across lanes) is then conflict-free, against 2x the ideal LDS
+    // cycles for padded 144-byte rows with the global unit order
+    // (scripts/lds_bank_model.py).
+    static constexpr bool SWZ = W16 && F::W == 4 && RS_LDS_SWZ;
+    static constexpr int ROW = SWZ ? TB : TB + RS_LDS_PAD;  // LDS row stride
     static constexpr int UB = W16 ? 8 * F::W : 4 * F::W;  // global bytes per unit
     static constexpr int U = TB / UB;                     // units per tile
     typedef typename F::Vec V;
+    __device__ static uint32_t swz(int row) {
+        const uint32_t r = (uint32_t)row;
+        return (((r & 1) ? 0x4u : 0u) ^ ((r & 4) ? 0x7u : 0u) ^ ((r & 8) ? 0xEu : 0u) ^ ((r & 16) ? 0xAu : 0u)) << 4;
+    }
+    // LDS byte offset of unit u's low (h = 0) or high (h = 1) half in `row`
+    __device__ static uint32_t loff(int row, int u, int h) {
+        if constexpr (SWZ) return ((uint32_t)row * TB + (uint32_t)u * 16 + 64u * h) ^ swz(row);
+        else return (uint32_t)(row * ROW + F::off(u) + 32 * h);
+    }
     __device__ static V get(const uint8_t *lds, int row, int u) {
         V v;
-        const uint8_t *p = lds + row * ROW + F::off(u);
         if constexpr (W16) {
-            ldw_lds<F::W>(p, v.l);
-            ldw_lds<F::W>(p + 32, v.h);
+            ldw_lds<F::W>(lds + loff(row, u, 0), v.l);
+            ldw_lds<F::W>(lds + loff(row, u, 1), v.h);
         } else {
-            ldw_lds<F::W>(p, v.b);
+            ldw_lds<F::W>(lds + loff(row, u, 0), v.b);
         }
         return v;
     }
     __device__ static void put(uint8_t *lds, int row, int u, const V &v) {
         typedef typename VecOf<F::W>::T T;
-        uint8_t *p = lds + row * ROW + F::off(u);
         auto st = [](uint8_t *q, const uint32_t(&w)[F::W]) {
             T x;
             if constexpr (F::W == 1) x = w[0];
@@ -1246,10 +1274,10 @@ struct LTile {
             *(__attribute__((address_space(3))) T *)(q) = x;
         };
         if constexpr (W16) {
-            st(p, v.l);
-            st(p + 32, v.h);
+            st(lds + loff(row, u, 0), v.l);
+            st(lds + loff(row, u, 1), v.h);
         } else {
-            st(p, v.b);
+            st(lds + loff(row, u, 0), v.b);
         }
     }
     // Unit u of the tile starting at byte `tile` exists in a row of S bytes.
@@ -1290,6 +1318,34 @@ __device__ __forceinline__ Need load_need(const uint32_t (&src)[8]) {
 #pragma unroll
     for (int k = 0; k < 8; k++) n.w[k] = __builtin_amdgcn_readfirstlane(src[k]);
     return n;
+}
+
+// Output index of revealed work row r, or -1: outputs are numbered as the
+// reconstruct plan lists them (codec.cpp: erased data shards = work rows
+// m.. first, then erased parity shards = rows 0..m-1), i.e. the rank of r
+// among the set bits of the revealed-row mask in the rotated order [m, n),
+// [0, m).  Replaces an LDS row -> output table (k_rec_lds then needs no LDS
+// beyond its 32 KB tile at n = 256).
+__device__ __forceinline__ int reveal_index(const Need &n, int m, int r) {
+    int below = 0, below_m = 0, total = 0;
+    const int wr = r >> 5;
+    uint32_t word = n.w[0];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int c = __builtin_popcount(n.w[k]);  // wave-uniform words: scalar counts
+        total += c;
+        if (k * 32 + 32 <= m) below_m += c;
+        else if (k * 32 < m) below_m += __builtin_popcount(n.w[k] & ((1u << (m & 31)) - 1));
+        below += k < wr ? c : 0;
+        if (k > 0) {
+            asm volatile("" : "+v"(word));  // a select chain, not a stack array (see rows_needed)
+            word = wr == k ? n.w[k] : word;
+        }
+    }
+    const uint32_t bit = 1u << (r & 31);
+    if (!(word & bit)) return -1;
+    below += __builtin_popcount(word & (bit - 1));
+    return r >= m ? below - below_m : total - below_m + below;
 }
 
 // Row sources / sinks of a pass: the LDS image by default; the first pass of
@@ -1382,13 +1438,14 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
 // first pass reads through `in`, the last writes through `out`.  A first pass
 // that does not read the LDS image runs every group (rows past mtrunc come in
 // as zero, and zero rows transform to zero rows): later passes read those rows.
-template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed>
+template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed, int P0 = 0>
 __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
                                               NeedT need, const In &in, const Out &out) {
     constexpr int N = 1 << LOGN, NP4 = LOGN / 2, NP = NP4 + (LOGN & 1);
     const LdsIO<F> lio{lds};
     cfor<NP>([=](auto PI) {  // by value: a captured reference to `need` kept it on the stack
         constexpr int p = decltype(PI)::value;
+        if constexpr (p >= P0) {  // passes before P0 were run by the caller (fused)
         constexpr bool radix4 = p < NP4;
         // IFFT: radix-4 passes at dist 4^p (groups N / (4 dist)), then radix-2 at dist N/2;
         // FFT: radix-4 passes at dist N / 4^(p+1) (groups 4^p), then radix-2 at dist 1
@@ -1403,7 +1460,16 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
         int active;
         if constexpr (radix4) {
             active = (mtrunc + 4 * dist - 1) / (4 * dist);
-            if (active > groups || from_hbm) active = groups;
+            if (active > groups) active = groups;
+            if constexpr (from_hbm && INV && p < NP - 1 && !RS_REC_NO_ZSKIP) {
+                // groups past mtrunc hold zero rows: zero their LDS rows instead
+                // of transforming them (the pass's barrier covers these stores)
+                const int z0 = active * 4 * dist;
+                for (int it = threadIdx.x; it < (N - z0) * LTile<F>::U; it += 256)
+                    lio(z0 + it / LTile<F>::U, it % LTile<F>::U, F::zero());
+            } else if constexpr (from_hbm) {
+                active = groups;
+            }
         } else {
             active = INV ? 1 : (mtrunc + 1) / 2 < N / 2 && !from_hbm ? (mtrunc + 1) / 2 : N / 2;
         }
@@ -1419,6 +1485,7 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
             run(lio, out);
         } else {
             run(lio, lio);
+        }
         }
     });
 }
@@ -1440,11 +1507,15 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     constexpr int N = 1 << LOGN, U = L::U;
     constexpr int K = (N * U + 255) / 256;  // derivative outputs per thread
     __shared__ __attribute__((aligned(16))) uint8_t lds[N * L::ROW];
+#if RS_REC_LDS_OUTROW
     __shared__ int outrow[N];  // work row -> output index (reveal), -1: not revealed
-    const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
     for (int r = threadIdx.x; r < N; r += 256) outrow[r] = -1;
     __syncthreads();
     for (int j = threadIdx.x; j < a.nd; j += 256) outrow[a.pos[j]] = j;  // read after the IFFT's barriers
+#else
+    const int *outrow = nullptr;  // output index from the revealed-row mask (RevealIndex)
+#endif
+    const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
     // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0
     struct ScaleIn {
         const RecArgs &a;
@@ -1467,8 +1538,13 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         const RecArgs &a;
         const int *outrow;
         uint64_t tile;
+        Need nw;
         __device__ void operator()(int r, int u, const V &x) const {
+#if RS_REC_LDS_OUTROW
             const int j = outrow[r];
+#else
+            const int j = reveal_index(nw, a.m, r);
+#endif
             if (j < 0 || !L::valid(tile, a.S, u)) return;
             V v = F::zero();
             F::mul_add(v, x, a.tw_out + (uint64_t)j * F::TWD);
@@ -1478,7 +1554,53 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     };
     const LdsIO<FT> lio{lds};
     lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile}, lio);
+    const Reveal rv{a, outrow, tile, load_need(a.need)};
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
+    if constexpr (LOGN >= 3 && !RS_REC_UNFUSED_DERIV) {
+        // fused with the FFT's first pass (radix-4 at dist D = N/4, one group,
+        // twiddle slot 0): a thread forms the derivative of its four rows
+        // i + aD from the IFFT image (the a-bit terms from the rows it holds),
+        // transforms them, and stores them after every thread has read.
+        constexpr int D = N / 4;
+        constexpr int KF = (D * U + 255) / 256;  // fused items per thread
+        V x[KF][4];
+#pragma unroll
+        for (int k = 0; k < KF; k++) {
+            const int it = threadIdx.x + 256 * k;
+            if (it < D * U) {
+                const int i = it / U, u = it - i * U;
+                V X[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) X[q] = L::get(lds, i + q * D, u);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    x[k][q] = X[q];
+                    if (!(q & 1)) F::xor_into(x[k][q], X[q | 1]);
+                    if (!(q & 2)) F::xor_into(x[k][q], X[q | 2]);
+                    for (int b = 1; b < D; b <<= 1)
+                        if (!(i & b)) F::xor_into(x[k][q], L::get(lds, (i | b) + q * D, u));
+                }
+                fft4<FT>(x[k][0], x[k][1], x[k][2], x[k][3], a.tw_fft);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KF; k++) {
+            const int it = threadIdx.x + 256 * k;
+            if (it < D * U) {
+                const int i = it / U, u = it - i * U;
+#pragma unroll
+                for (int q = 0; q < 4; q++) L::put(lds, i + q * D, u, x[k][q]);
+            }
+        }
+        __syncthreads();
+        if (a.prune) {
+            lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, Need, 1>(lds, a.mtrunc, a.tw_fft, load_need(a.need), lio, rv);
+        } else {
+            lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NoNeed, 1>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
+        }
+        return;
+    }
     {
         V o[K];
 #pragma unroll
@@ -1502,7 +1624,6 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         }
         __syncthreads();
     }
-    const Reveal rv{a, outrow, tile};
     if (a.prune) {
         lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, load_need(a.need), lio, rv);
     } else {

@@ -81,6 +81,7 @@ struct RecArgs {
     const uint32_t *tw_fft;     // decoder FFT schedule (fft_slots(logn) tables)
     uint64_t S;
     int mtrunc;                 // m + k
+    int m;                      // work rows before the data rows (outputs: data rows m.., then parity rows 0..)
     int nd;
     // errorBitfield analog (leopard16.go:1076-1252): bit r set when work row r
     // is revealed; FFT groups whose rows are all unset are skipped.

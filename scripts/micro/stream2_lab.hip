@@ -202,6 +202,14 @@ int main() {
     rep("contig d1", timeit([&] { hipLaunchKernelGGL((k_stream<1, 1, false>), dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
     rep("contig d1 bar", timeit([&] { hipLaunchKernelGGL((k_stream<1, 1, true>), dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
     rep("regs d1 grid1024", timeit([&] { hipLaunchKernelGGL((k_stream<0, 1, false>), dim3(1024), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
+    // row stride padding: rows exactly 1 MiB apart alias in the low 20 address bits
+    for (uint32_t pad : {256u, 2048u, 4096u, 8192u, 65536u}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "regs d1 rowpad %u", pad);
+        const uint32_t RSp = (uint32_t)S + pad;
+        const uint64_t SSp = (uint64_t)(K + P) * RSp;
+        rep(nm, timeit([&] { hipLaunchKernelGGL((k_stream<0, 1, false>), dim3(512), dim3(256), 0, 0, base, sink, RSp, TS, SSp); }));
+    }
     {
         const size_t half = bytes / 2, n16 = half / 16;
         for (int g : {2048, 4096, 8192, 16384}) {
