@@ -1193,6 +1193,13 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 // tile must cover whole 64-byte blocks (low bytes [0,32), high bytes
 // [32,64)), so W = 1 (32-byte tiles) is invalid: the parity tests reject it.
 constexpr uint64_t kLdsMinGrid = 512;
+#ifndef RS_ENC_ACC_REGS
+#define RS_ENC_ACC_REGS 1  // k_enc_lds keeps the accumulator in registers (even log m); 0: in LDS
+#endif
+#ifndef RS_ENC_LDS_MINBLK
+#define RS_ENC_LDS_MINBLK 4  // k_enc_lds occupancy hint: 4 workgroups per CU (<= 128 VGPRs)
+#endif
+constexpr bool enc_acc_regs(int logm) { return RS_ENC_ACC_REGS && logm % 2 == 0 && logm >= 4; }
 #ifndef RS_REC_LDS_OUTROW
 #define RS_REC_LDS_OUTROW 0  // 1: reveal through an LDS row -> output table (1 KB more LDS per workgroup)
 #endif
@@ -1438,14 +1445,14 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
 // first pass reads through `in`, the last writes through `out`.  A first pass
 // that does not read the LDS image runs every group (rows past mtrunc come in
 // as zero, and zero rows transform to zero rows): later passes read those rows.
-template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed, int P0 = 0>
+template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed, int P0 = 0, int P1 = 32>
 __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
                                               NeedT need, const In &in, const Out &out) {
     constexpr int N = 1 << LOGN, NP4 = LOGN / 2, NP = NP4 + (LOGN & 1);
     const LdsIO<F> lio{lds};
     cfor<NP>([=](auto PI) {  // by value: a captured reference to `need` kept it on the stack
         constexpr int p = decltype(PI)::value;
-        if constexpr (p >= P0) {  // passes before P0 were run by the caller (fused)
+        if constexpr (p >= P0 && p < P1) {  // passes outside [P0, P1) are run by the caller (fused)
         constexpr bool radix4 = p < NP4;
         // IFFT: radix-4 passes at dist 4^p (groups N / (4 dist)), then radix-2 at dist N/2;
         // FFT: radix-4 passes at dist N / 4^(p+1) (groups 4^p), then radix-2 at dist 1
@@ -1637,12 +1644,13 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
 // into acc (chunk 0: writes acc), and the FFT's last pass writes the parity
 // rows (or compares them, verify).
 template <class F, int LOGM, bool VERIFY>
-__global__ void __launch_bounds__(256) k_enc_lds(EncodeArgs a) {
+__global__ void __launch_bounds__(256, RS_ENC_LDS_MINBLK) k_enc_lds(EncodeArgs a) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
     constexpr int M = 1 << LOGM;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-    uint8_t *acc = lds_dyn, *cur = lds_dyn + M * L::ROW;
+    constexpr bool ACCR = enc_acc_regs(LOGM);
+    uint8_t *acc = lds_dyn, *cur = ACCR ? lds_dyn : lds_dyn + M * L::ROW;
     const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
     const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
     constexpr int its = ifft_slot_count(LOGM);
@@ -1674,6 +1682,60 @@ __global__ void __launch_bounds__(256) k_enc_lds(EncodeArgs a) {
             else F::store(prow, u, v);
         }
     };
+    if constexpr (ACCR) {
+        // acc in registers: the IFFT's last pass and the FFT's first are both
+        // one radix-4 group at dist D = M/4 with the same item -> (rows, unit)
+        // mapping, so a thread keeps acc rows i + qD of its items across the
+        // chunks and the LDS holds only the current chunk.
+        constexpr int NP = LOGM / 2, D = M / 4;
+        constexpr int KF = (D * L::U + 255) / 256;  // items per thread
+        constexpr int last = [] {  // twiddle slot of the IFFT's last pass
+            int sl = 0;
+            for (int q = 0; q < NP - 1; q++) sl += 3 * (M / (4 << (2 * q)));
+            return sl;
+        }();
+        V ar[KF][4];
+        for (int c = 0; c < a.nchunks; c++) {
+            const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
+            const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
+            const ChunkIn in{a, row0, cnt, soff, tile};
+            const LdsIO<F> lio{cur};
+            lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, NP - 1>(cur, cnt, tw, NoNeed{}, in, lio);
+#pragma unroll
+            for (int k = 0; k < KF; k++) {
+                const int it = threadIdx.x + 256 * k;
+                if (it < D * L::U) {
+                    const int i = it / L::U, u = it - i * L::U;
+                    V x[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) x[q] = L::get(cur, i + q * D, u);
+                    ifft4<F>(x[0], x[1], x[2], x[3], tw + (uint64_t)last * F::TWD);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (c == 0) ar[k][q] = x[q];
+                        else F::xor_into(ar[k][q], x[q]);
+                    }
+                }
+            }
+            __syncthreads();  // the next chunk's first pass overwrites cur
+        }
+        uint32_t bad = 0;
+#pragma unroll
+        for (int k = 0; k < KF; k++) {
+            const int it = threadIdx.x + 256 * k;
+            if (it < D * L::U) {
+                const int i = it / L::U, u = it - i * L::U;
+                fft4<F>(ar[k][0], ar[k][1], ar[k][2], ar[k][3], a.tw_fft);
+#pragma unroll
+                for (int q = 0; q < 4; q++) L::put(cur, i + q * D, u, ar[k][q]);
+            }
+        }
+        __syncthreads();
+        lds_transform<F, false, LOGM, LdsIO<F>, ParityOut, NoNeed, 1>(cur, a.p, a.tw_fft, NoNeed{}, LdsIO<F>{cur},
+                                                                       ParityOut{a, soff, tile, &bad});
+        if constexpr (VERIFY) flag_mismatch(a.mismatch, bad != 0);
+        return;
+    }
     for (int c = 0; c < a.nchunks; c++) {
         const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
         const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
@@ -1966,7 +2028,7 @@ hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
 template <class F, int LOGM>
 hipError_t enc_lds_t(bool verify, const EncodeArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)((a.shard_size + LTile<F>::TB - 1) / LTile<F>::TB), (unsigned)a.nstripes);
-    const size_t lds = (size_t)2 * (1 << LOGM) * LTile<F>::ROW;
+    const size_t lds = (size_t)(enc_acc_regs(LOGM) ? 1 : 2) * (1 << LOGM) * LTile<F>::ROW;
     if (verify) {
         (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL((k_enc_lds<F, LOGM, true>), grid, dim3(256), lds, s, a);

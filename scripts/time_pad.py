@@ -40,7 +40,7 @@ def main():
             view = buf.as_strided((B, k + p, S), (SS, RS, 1))
             g.manual_seed(0x5EED)
             view.copy_(torch.randint(0, 256, (B, k + p, S), dtype=torch.uint8, device="cuda", generator=g))
-            for _ in range(5):
+            for _ in range(20):
                 c.encode_dev_batch(view, st)
             torch.cuda.synchronize()
             par = view[:, k:].contiguous()

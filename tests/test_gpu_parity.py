@@ -6,6 +6,8 @@ seconds; at the BASELINE configs' full sizes, size-independent properties
 shard columns are independent, so any 64-byte-aligned byte window of the GPU
 output must equal the oracle run on that window of the input).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -243,6 +245,26 @@ def test_baseline_c3_full_oracle(torch_dev):
     rs.New16(k, p).encode_dev(slab)
     torch.cuda.synchronize()
     assert np.array_equal(slab[k:].cpu().numpy(), ref)
+
+
+def test_baseline_c5_full_port(torch_dev):
+    """C5 (1024+256 x 256 KiB, m = 256: the LDS-resident encode) bit-exact over
+    the whole stripe against the AVX2 port of the reference encode, which
+    tests/test_oracle.py pins to the scalar oracle (including 1024+256)."""
+    if not orc.simd_available():
+        pytest.skip("no AVX2 on this host")
+    torch = torch_dev
+    k, p, S = 1024, 256, 256 << 10
+    rng = np.random.default_rng(0xC5)
+    data = rand_data(rng, k, S)
+    ref = orc.encode_simd(k, p, data, min(16, os.cpu_count() or 1))
+    slab = torch.zeros((k + p, S), dtype=torch.uint8, device="cuda")
+    slab[:k] = torch.from_numpy(data).cuda()
+    c = rs.New16(k, p)
+    c.encode_dev(slab)
+    torch.cuda.synchronize()
+    assert np.array_equal(slab[k:].cpu().numpy(), ref)
+    assert c.verify_dev(slab)
 
 
 def test_baseline_c4_reconstruct(torch_dev):
