@@ -22,6 +22,7 @@ from .codec import (  # noqa: F401
     ErrPanic,
     ErrDevice,
     alloc_pinned,
+    EmptyShard,
 )
 from ._capi import LIB_PATH, lib  # noqa: F401
 
@@ -29,4 +30,5 @@ __all__ = [
     "New", "New8", "New16", "ReedSolomon", "RSError", "ErrInvShardNum", "ErrMaxShardNum", "ErrTooFewShards",
     "ErrShardNoData", "ErrShardSize", "ErrInvalidShardSize", "ErrNotSupported", "ErrShortData",
     "ErrReconstructRequired", "ErrPanic", "ErrDevice", "LIB_PATH", "lib", "alloc_pinned",
+    "EmptyShard",
 ]

@@ -99,6 +99,34 @@ def alloc_pinned(nbytes: int) -> np.ndarray:
     return a
 
 
+class EmptyShard:
+    """A missing shard that keeps its memory, like Go's ``shards[i][:0]``:
+    length 0 (so Reconstruct treats it as missing) and capacity ``len(buf)``.
+    When the capacity holds the shard size, Reconstruct writes the rebuilt
+    shard into ``buf`` (leopard16.go:556-560, ``shards[i][0:shardSize]``) --
+    e.g. straight into an alloc_aligned(pinned=True) row -- instead of
+    allocating a new array."""
+
+    __slots__ = ("buf",)
+
+    def __init__(self, buf):
+        self.buf = buf
+
+    def __len__(self) -> int:
+        return 0
+
+
+def _capacity_view(s, S: int):
+    """Go's cap() check for a missing shard: the EmptyShard's buffer, if it is
+    a C-contiguous uint8 array of at least S bytes; None otherwise."""
+    if not isinstance(s, EmptyShard):
+        return None
+    b = s.buf
+    if not isinstance(b, np.ndarray) or b.dtype != np.uint8 or not b.flags["C_CONTIGUOUS"] or b.nbytes < S:
+        return None
+    return b.reshape(-1)[:S]
+
+
 def _host_rows(shards: Sequence):
     n = len(shards)
     ptrs = (C.c_void_p * n)()
@@ -260,7 +288,11 @@ class ReedSolomon:
         bufs = list(shards)
         for i in range(min(end, total)):
             if bufs[i] is None or len(bufs[i]) == 0:
-                bufs[i] = np.empty(S, dtype=np.uint8)  # Go: make([]byte, shardSize); fully overwritten
+                # Go: shards[i][0:shardSize] when cap(shards[i]) >= shardSize, else
+                # make([]byte, shardSize) (leopard16.go:556-560); fully overwritten
+                bufs[i] = _capacity_view(bufs[i], S)
+                if bufs[i] is None:
+                    bufs[i] = np.empty(S, dtype=np.uint8)
         ptrs = (C.c_void_p * total)()
         lens = (C.c_size_t * total)()
         for i, s in enumerate(shards):

@@ -478,6 +478,39 @@ def test_host_reconstruct_c4_output_memory(outputs):
         assert np.array_equal(outs[i], full[i]), i
 
 
+# The Python mirror's Go-capacity form: a missing shard passed as
+# EmptyShard(row) (Go: shards[i][:0] of an AllocAligned row) is rebuilt into
+# that row -- pinned here, so the copy-out is direct -- and the list entry
+# becomes that same memory; a plain empty array still gets a new array (Go's make).
+def test_host_reconstruct_into_capacity():
+    k, p, S = 128, 32, 1 << 18
+    c = rs.New16(k, p)
+    shards = c.alloc_aligned(S, pinned=True)
+    rng = np.random.default_rng(5)
+    for i in range(k):
+        shards[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+    c.encode(shards)
+    full = [s.copy() for s in shards]
+    er = sorted(rng.choice(k + p, p, replace=False).tolist())
+    rows = {i: shards[i] for i in er}
+    for i in er:
+        rows[i][:] = 0x5A
+    work = list(shards)
+    for j, i in enumerate(er):
+        work[i] = rs.EmptyShard(rows[i]) if j % 2 == 0 else np.zeros(0, np.uint8)
+    c.reconstruct(work)
+    for j, i in enumerate(er):
+        assert np.array_equal(work[i], full[i]), i
+        same = work[i].ctypes.data == rows[i].ctypes.data
+        assert same == (j % 2 == 0), i
+    # a capacity smaller than the shard size is not used (Go: make)
+    work = [f.copy() for f in full]
+    small = np.zeros(S // 2, np.uint8)
+    work[er[0]] = rs.EmptyShard(small)
+    c.reconstruct(work)
+    assert np.array_equal(work[er[0]], full[er[0]]) and not np.any(small)
+
+
 # Codec scratch shared across caller streams: device-resident encodes return
 # before their kernels finish, so a second call on another stream must not
 # overwrite the row-pointer table (non-strided rows) or the multi-pass work
