@@ -1196,8 +1196,11 @@ constexpr uint64_t kLdsMinGrid = 512;
 #ifndef RS_ENC_ACC_REGS
 #define RS_ENC_ACC_REGS 1  // k_enc_lds keeps the accumulator in registers (even log m); 0: in LDS
 #endif
+#ifndef RS_ENC_PREFETCH
+#define RS_ENC_PREFETCH 0  // 1: k_enc_lds prefetches the next chunk's first-pass rows into registers (measured slower: 3 waves/SIMD)
+#endif
 #ifndef RS_ENC_LDS_MINBLK
-#define RS_ENC_LDS_MINBLK 4  // k_enc_lds occupancy hint: 4 workgroups per CU (<= 128 VGPRs)
+#define RS_ENC_LDS_MINBLK (RS_ENC_PREFETCH ? 3 : 4)  // k_enc_lds occupancy hint (workgroups per CU): 4 = <= 128 VGPRs
 #endif
 constexpr bool enc_acc_regs(int logm) { return RS_ENC_ACC_REGS && logm % 2 == 0 && logm >= 4; }
 #ifndef RS_REC_LDS_OUTROW
@@ -1378,6 +1381,18 @@ __device__ __forceinline__ void cfor(Fn &&f) {
     cfor_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+// Barrier between LDS passes: LDS-only (s_waitcnt lgkmcnt(0); s_barrier), so
+// global loads a kernel has in flight (the encoder's next-chunk prefetch) are
+// not drained at every pass as __syncthreads() would.  The passes communicate
+// only through LDS; global stores are never read back inside a launch.
+__device__ __forceinline__ void lds_sync() {
+#if RS_ENC_PREFETCH
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+    __syncthreads();  // the measured default (no loads to keep in flight)
+#endif
+}
+
 // One radix-4 pass (rows i, i+d, i+2d, i+3d; twiddles m01, m02, m23 at
 // tw + 3*g) over the active groups, or a radix-2 pass.  in(row, u) supplies
 // the rows, out(row, u, v) takes the results.
@@ -1436,7 +1451,7 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
         }
     }
 #ifndef RS_LDS_ABL_NOBAR  // ablation: wrong results, measures the barrier cost
-    __syncthreads();
+    lds_sync();
 #endif
 }
 
@@ -1695,12 +1710,54 @@ __global__ void __launch_bounds__(256, RS_ENC_LDS_MINBLK) k_enc_lds(EncodeArgs a
             return sl;
         }();
         V ar[KF][4];
+#if RS_ENC_PREFETCH
+        // the IFFT's first pass (radix-4 at dist 1, groups of rows 4g..4g+3,
+        // lane-varying twiddles) runs here: its rows for chunk c + 1 are loaded
+        // into registers while chunk c's LDS passes run (LDS-only barriers
+        // leave the loads in flight)
+        constexpr int G0 = M / 4, KP = (G0 * L::U + 255) / 256;
+        V pf[KP][4];
+        auto prefetch = [&](int c) {
+            const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
+#pragma unroll
+            for (int k = 0; k < KP; k++) {
+                const int it = threadIdx.x + 256 * k;
+                if (it < G0 * L::U) {
+                    const int g = it / L::U, u = it - g * L::U;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int r = 4 * g + q;
+                        pf[k][q] = r < cnt && L::valid(tile, a.shard_size, u)
+                                       ? F::load(row_ptr(a.data, row0 + r) + soff + tile, u)
+                                       : F::zero();
+                    }
+                }
+            }
+        };
+        prefetch(0);
+#endif
         for (int c = 0; c < a.nchunks; c++) {
             const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
             const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
-            const ChunkIn in{a, row0, cnt, soff, tile};
             const LdsIO<F> lio{cur};
+#if RS_ENC_PREFETCH
+#pragma unroll
+            for (int k = 0; k < KP; k++) {
+                const int it = threadIdx.x + 256 * k;
+                if (it < G0 * L::U) {
+                    const int g = it / L::U, u = it - g * L::U;
+                    ifft4<F, kLdsBranchFree>(pf[k][0], pf[k][1], pf[k][2], pf[k][3], tw + (uint64_t)g * 3 * F::TWD);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) L::put(cur, 4 * g + q, u, pf[k][q]);
+                }
+            }
+            if (c + 1 < a.nchunks) prefetch(c + 1);
+            lds_sync();
+            lds_transform<F, true, LOGM, LdsIO<F>, LdsIO<F>, NoNeed, 1, NP - 1>(cur, cnt, tw, NoNeed{}, lio, lio);
+#else
+            const ChunkIn in{a, row0, cnt, soff, tile};
             lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, NP - 1>(cur, cnt, tw, NoNeed{}, in, lio);
+#endif
 #pragma unroll
             for (int k = 0; k < KF; k++) {
                 const int it = threadIdx.x + 256 * k;
@@ -1717,7 +1774,7 @@ __global__ void __launch_bounds__(256, RS_ENC_LDS_MINBLK) k_enc_lds(EncodeArgs a
                     }
                 }
             }
-            __syncthreads();  // the next chunk's first pass overwrites cur
+            lds_sync();  // the next chunk's first pass overwrites cur
         }
         uint32_t bad = 0;
 #pragma unroll
