@@ -547,7 +547,8 @@ def test_device_encode_two_streams(torch_dev, bits, k, p, S, layout):
 # register units, at sizes the oracle finishes in seconds.
 @pytest.mark.parametrize("width", ["narrow", "wide"])
 @pytest.mark.parametrize("bits,k,p,S", [(8, 10, 4, 4096), (8, 100, 28, 4096 + 192), (16, 100, 28, 4096 + 192),
-                                        (16, 70, 40, 2048), (8, 70, 40, 2048), (16, 128, 32, 4096 + 640)])
+                                        (16, 70, 40, 2048), (8, 70, 40, 2048), (16, 128, 32, 4096 + 640),
+                                        (16, 100, 100, 2048), (8, 100, 100, 2048), (16, 700, 200, 1024)])
 def test_unit_width_variants(monkeypatch, width, bits, k, p, S):
     monkeypatch.setenv("RS_UNIT_WIDTH", width)
     monkeypatch.setenv("RS_BS", "0")
