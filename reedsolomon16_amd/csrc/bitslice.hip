@@ -228,6 +228,15 @@ __device__ __forceinline__ void hp_get(uint32_t lbase, int row, Half &v) {
 // release/acquire fence, which waits for every outstanding global load
 // (vmcnt(0)) and so would drain the next chunk's prefetch at the first
 // barrier of every chunk; this waits for LDS traffic alone.
+// Cache-policy bits of the data-row loads and parity stores (buffer
+// instruction aux: 1 = sc0, 2 = nt, 16 = sc1; MI355X_MICROARCH.md stores
+// table).  0 = default policy; other values are A/B experiments.
+#ifndef RS_BS_LOAD_AUX
+#define RS_BS_LOAD_AUX 0
+#endif
+#ifndef RS_BS_STORE_AUX
+#define RS_BS_STORE_AUX 0
+#endif
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int LOGM, bool VERIFY>
@@ -294,7 +303,7 @@ struct HpEncoder {
             const uint32_t soff = (uint32_t)(M * c + RW * w + i) * (uint32_t)a.row_stride;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * QS, soff, 0);
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * QS, soff, RS_BS_LOAD_AUX);
                 uint32_t *d = q < 2 ? &St[i][q * 4] : &St[HR + i][(q - 2) * 4];
                 d[0] = x[0], d[1] = x[1], d[2] = x[2], d[3] = x[3];
             }
@@ -464,7 +473,7 @@ struct HpEncoder {
 #if defined(RS_BS_ABL_NOSTORE)
                             asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
 #else
-                            __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * QS, soff, 0);
+                            __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * QS, soff, RS_BS_STORE_AUX);
 #endif
                         }
                     }
