@@ -14,10 +14,10 @@ run() {  # name, counters, command...
   local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -3 $OUT/$name.err; exit $rc; }
 }
 for W in C3; do
-  run ${W}_p1 "$P1" python3 bench.py --no-cpu --no-single --steps 20 --warmup 3
-  run ${W}_p2 "$P2" python3 bench.py --no-cpu --no-single --steps 20 --warmup 3
-  run ${W}_fetch FETCH_SIZE python3 bench.py --no-cpu --no-single --steps 20 --warmup 3
-  run ${W}_write WRITE_SIZE python3 bench.py --no-cpu --no-single --steps 20 --warmup 3
+  run ${W}_p1 "$P1" python3 bench.py --no-cpu --no-single --no-unpadded --stripes 32 --steps 20 --warmup 3
+  run ${W}_p2 "$P2" python3 bench.py --no-cpu --no-single --no-unpadded --stripes 32 --steps 20 --warmup 3
+  run ${W}_fetch FETCH_SIZE python3 bench.py --no-cpu --no-single --no-unpadded --stripes 32 --steps 20 --warmup 3
+  run ${W}_write WRITE_SIZE python3 bench.py --no-cpu --no-single --no-unpadded --stripes 32 --steps 20 --warmup 3
 done
 timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/lds_trace -o run -- python3 scripts/time_ops.py --configs C4,C4e1,C5,C5x8 --iters 30 > $OUT/lds_trace.out 2> $OUT/lds_trace.err
 rc=$?; echo "lds trace rc=$rc"; [ $rc -eq 0 ] || { tail -3 $OUT/lds_trace.err; exit $rc; }
