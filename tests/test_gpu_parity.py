@@ -36,7 +36,7 @@ ENCODE_CASES = [
     (2, 1, 64), (3, 1, 128), (4, 2, 256), (10, 4, 1024), (5, 3, 64), (8, 4, 192), (16, 4, 320),
     (10, 6, 128), (20, 8, 64), (33, 17, 128), (100, 28, 64), (128, 32, 256), (130, 32, 64),
     (3, 7, 64), (1, 1, 64), (1, 5, 64), (37, 9, 64), (128, 128, 128), (200, 100, 64),
-    (70, 40, 128), (300, 64, 64), (64, 65, 64),
+    (70, 40, 128), (300, 64, 64), (64, 65, 64), (100, 150, 128), (16, 200, 64),
 ]
 
 
