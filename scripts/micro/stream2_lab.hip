@@ -159,6 +159,21 @@ __global__ void __launch_bounds__(256, 2) k_dma(uint8_t *base, uint32_t *sink, u
 __global__ void __launch_bounds__(256) k_copy(const u32x4 *src, u32x4 *dst, size_t n16) {
     for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
 }
+// Calibration: copy with U float4 per thread per iteration (a wave moves
+// U KiB per step, each lane's U pieces 1 KiB apart), half the bytes read
+// and half written, as the guide's "float4 copy" figure.
+template <int U>
+__global__ void __launch_bounds__(256) k_copyu(const u32x4 *src, u32x4 *dst, size_t n16) {
+    const size_t step = (size_t)gridDim.x * 256 * U;
+    for (size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x; i < n16; i += step) {
+        u32x4 v[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) v[j] = i + 256 * j < n16 ? src[i + 256 * j] : u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            if (i + 256 * j < n16) dst[i + 256 * j] = v[j];
+    }
+}
 // Calibration: plain grid-stride float4 read (XOR fold, one store per thread).
 __global__ void __launch_bounds__(256) k_read(const u32x4 *src, uint32_t *sink, size_t n16) {
     u32x4 a = {0, 0, 0, 0};
@@ -216,6 +231,13 @@ int main() {
             char nm[64];
             snprintf(nm, sizeof nm, "copy grid %d", g);
             rep(nm, timeit([&] { hipLaunchKernelGGL(k_copy, dim3(g), dim3(256), 0, 0, (const u32x4 *)base, (u32x4 *)(base + half), n16); }));
+        }
+        for (int g : {1024, 2048, 4096}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "copy x4 grid %d", g);
+            rep(nm, timeit([&] { hipLaunchKernelGGL(k_copyu<4>, dim3(g), dim3(256), 0, 0, (const u32x4 *)base, (u32x4 *)(base + half), n16); }));
+            snprintf(nm, sizeof nm, "copy x8 grid %d", g);
+            rep(nm, timeit([&] { hipLaunchKernelGGL(k_copyu<8>, dim3(g), dim3(256), 0, 0, (const u32x4 *)base, (u32x4 *)(base + half), n16); }));
         }
         for (int g : {2048, 8192}) {
             char nm[64];
