@@ -95,6 +95,67 @@ __global__ void __launch_bounds__(256, 2) k_stream(uint8_t *base, uint32_t *sink
 }
 
 
+
+// Deferred parity stores: tile t's 16 parity stores are issued 4 per chunk
+// during tile t + grid's chunk loop (pend holds them), instead of as one burst
+// at the end of tile t.  LAYOUT 0, DEPTH 1.
+__global__ void __launch_bounds__(256, 2) k_stream_defer(uint8_t *base, uint32_t *sink, uint32_t RS, uint32_t TS, uint64_t SS) {
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5, blk = lane & 31;
+    constexpr int TPS = S / 2048, NT = TPS * NST;
+    uint32_t St[64], acc[64], pend[64];
+    auto stage = [&](int tile, int c) {
+        const int stripe = tile / TPS, ct = tile % TPS;
+        const bool live = tile < NT;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            base + (live ? (size_t)stripe * SS : 0), 0, live ? (int)(K * RS + TPS * TS) : 0, 0x00020000);
+        uint32_t voff = ct * TS + blk * 64 + 4 * h * RS;
+        asm volatile("" : "+v"(voff));
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * 16, (uint32_t)(32 * c + 8 * w + i) * RS, 0);
+                St[16 * i + 4 * q] = x[0], St[16 * i + 4 * q + 1] = x[1], St[16 * i + 4 * q + 2] = x[2], St[16 * i + 4 * q + 3] = x[3];
+            }
+    };
+    auto store_part = [&](int ptile, int i) {  // parity row 8w + i of tile ptile from pend
+        if (ptile < 0) return;
+        const int stripe = ptile / TPS, ct = ptile % TPS;
+        const __amdgpu_buffer_rsrc_t ps = __builtin_amdgcn_make_buffer_rsrc(
+            base + (size_t)stripe * SS + (size_t)K * RS, 0, (int)(P * RS + TPS * TS), 0x00020000);
+        const uint32_t voff = ct * TS + blk * 64 + 4 * h * RS;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const u32x4 v = u32x4{pend[16 * i + 4 * q], pend[16 * i + 4 * q + 1], pend[16 * i + 4 * q + 2], pend[16 * i + 4 * q + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + q * 16, (uint32_t)(8 * w + i) * RS, 0);
+        }
+    };
+    int tile = blockIdx.x, ptile = -1;
+    stage(tile, 0);
+    for (; tile < NT; tile += gridDim.x) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+#pragma unroll
+            for (int j = 0; j < 64; j++) {
+                if (c == 0) acc[j] = St[j];
+                else acc[j] ^= St[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 64; j++) asm volatile("" : "+v"(acc[j])::"memory");
+            const int nc = c + 1;
+            stage(nc < 4 ? tile : tile + gridDim.x, nc % 4);
+            store_part(ptile, c);
+        }
+#pragma unroll
+        for (int j = 0; j < 64; j++) pend[j] = acc[j];
+        ptile = tile;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) store_part(ptile, i);
+    (void)sink;
+}
+
 typedef __attribute__((address_space(3))) void lvoid_t;
 typedef __attribute__((address_space(3))) u32x4 lds_u4;
 // LDS-DMA staging: each wave streams its 16 KB chunk (4 rows x 2 KB... as 16
@@ -217,6 +278,13 @@ int main() {
     rep("contig d1", timeit([&] { hipLaunchKernelGGL((k_stream<1, 1, false>), dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
     rep("contig d1 bar", timeit([&] { hipLaunchKernelGGL((k_stream<1, 1, true>), dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
     rep("regs d1 grid1024", timeit([&] { hipLaunchKernelGGL((k_stream<0, 1, false>), dim3(1024), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
+    rep("defer d1", timeit([&] { hipLaunchKernelGGL(k_stream_defer, dim3(512), dim3(256), 0, 0, base, sink, RS, TS, SS); }));
+    {
+        const uint32_t RSp = (uint32_t)S + 3072;
+        const uint64_t SSp = (uint64_t)(K + P) * RSp;
+        rep("regs d1 rowpad 3072", timeit([&] { hipLaunchKernelGGL((k_stream<0, 1, false>), dim3(512), dim3(256), 0, 0, base, sink, RSp, TS, SSp); }));
+        rep("defer d1 rowpad 3072", timeit([&] { hipLaunchKernelGGL(k_stream_defer, dim3(512), dim3(256), 0, 0, base, sink, RSp, TS, SSp); }));
+    }
     // row stride padding: rows exactly 1 MiB apart alias in the low 20 address bits
     for (uint32_t pad : {256u, 2048u, 4096u, 8192u, 65536u}) {
         char nm[64];
