@@ -154,6 +154,19 @@ int rs_verify_dev(rs_codec *codec, uint8_t *const *d_shards, size_t shard_size, 
 int rs_reconstruct_dev(rs_codec *codec, uint8_t *const *d_shards, const uint8_t *present, size_t shard_size,
                        int recover_all, void *stream);
 
+/* Batched device reconstruct with ONE erasure pattern (the usual repair after
+ * a lost device: every stripe misses the same shard indices): nstripes
+ * stripes, shard i of stripe z at base + z*stripe_stride + i*row_stride, all
+ * rebuilt in place in one launch (the LDS-resident kernel, grid.y = stripe)
+ * for codecs whose decode transform has n <= 256, stripe by stripe otherwise.
+ * Per stripe it is leopardFF16/FF8.Reconstruct (recover_all != 0) or
+ * ReconstructData (leopard16.go:351-358, leopard8.go:392-407) on that
+ * stripe's rows; present[] has k+p entries.  Same error rules and stream
+ * semantics as rs_reconstruct_dev.  row_stride >= shard_size; stripe_stride
+ * >= (k+p)*row_stride when nstripes > 1. */
+int rs_reconstruct_dev_batch(rs_codec *codec, uint8_t *base, size_t row_stride, size_t stripe_stride, size_t nstripes,
+                             const uint8_t *present, size_t shard_size, int recover_all, void *stream);
+
 /* Batched device encode of `nstripes` independent stripes laid out as one slab
  * per stripe: stripe j, shard i at d_base + j*stripe_stride + i*row_stride.
  * Asynchronous on `stream`. */

@@ -434,6 +434,23 @@ class ReedSolomon:
         pr = (C.c_uint8 * self.total_shards())(*[1 if x else 0 for x in present])
         _check(self._L.rs_reconstruct_dev(self._h, ptrs, pr, S, int(recover_all), _stream_handle(stream)))
 
+    def reconstruct_dev_batch(self, slab, present: Sequence[bool], recover_all: bool = True, stream=None) -> None:
+        """Rebuild the missing shards of every stripe of a [nstripes, k+p, S]
+        uint8 CUDA tensor in place, all with the same erasure pattern
+        (`present`, k+p flags), in one launch (rs_reconstruct_dev_batch).  Any
+        view with contiguous rows works; stripe and row strides come from the
+        tensor."""
+        if slab.dim() != 3 or slab.shape[1] != self.total_shards():
+            raise TypeError("slab must be a [nstripes, k+p, S] uint8 CUDA tensor")
+        if not slab.is_cuda or slab.dtype.itemsize != 1 or slab.stride(2) != 1:
+            raise TypeError("slab rows must be contiguous uint8 on a CUDA device")
+        if len(present) != self.total_shards():
+            raise ErrTooFewShards("need %d present flags, got %d" % (self.total_shards(), len(present)))
+        n, _, S = slab.shape
+        pr = (C.c_uint8 * len(present))(*[1 if x else 0 for x in present])
+        _check(self._L.rs_reconstruct_dev_batch(self._h, slab.data_ptr(), slab.stride(1), slab.stride(0), n, pr, S,
+                                                int(recover_all), _stream_handle(stream)))
+
     def encode_dev_batch(self, slab, stream=None) -> None:
         """Encode a [nstripes, k+p, S] uint8 CUDA tensor in one launch.  Any
         view whose rows are contiguous works (stride(2) == 1): stripe and row

@@ -1390,6 +1390,65 @@ int rs_verify_dev(rs_codec *c, uint8_t *const *d, size_t S, int *ok, void *strea
     return RS_OK;
 }
 
+int rs_reconstruct_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size_t stripe_stride, size_t nstripes,
+                             const uint8_t *present, size_t S, int recover_all, void *stream) {
+    if (!c || !base || !present || nstripes == 0 || nstripes > (size_t)INT32_MAX) return RS_ERR_INVALID_ARG;
+    std::vector<uint8_t> pr(present, present + c->total);
+    int np = 0, dp = 0;
+    for (int i = 0; i < c->total; i++)
+        if (pr[i]) {
+            np++;
+            if (i < c->k) dp++;
+        }
+    if (np == 0 || S == 0) return RS_ERR_SHARD_NO_DATA;
+    if (np == c->total || (!recover_all && dp == c->k)) return RS_OK;
+    if (np < c->k) return RS_ERR_TOO_FEW_SHARDS;
+    if (S % 64) return RS_ERR_INVALID_SHARD_SIZE;
+    if (row_stride < S || (nstripes > 1 && stripe_stride < (size_t)c->total * row_stride)) return RS_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (int ie = ensure_device(c)) return ie;
+    const hipStream_t s = pick_stream(c, stream);
+    if (int e = build_decode_plan(c)) return e;
+    if (c->dec_ok && c->logn <= kMaxLdsLogN) {
+        // one launch: grid.y = stripe, the pattern's tables shared (dev_plan cache)
+        DevPlan *dpl = nullptr;
+        if (int e = dev_plan(c, pr, recover_all != 0, &dpl)) return e;
+        const int nd = (int)dpl->pl.dst_shard.size();
+        if (nd) {
+            RecArgs ra{};
+            ra.pos = dpl->pos;
+            ra.tw_in = dpl->tw_in;
+            ra.tw_out = dpl->tw_out;
+            ra.tw_ifft = c->dtw_ifft.p;
+            ra.tw_fft = c->dtw_fft.p;
+            ra.S = S;
+            ra.mtrunc = c->m + c->k;
+            ra.m = c->m;
+            ra.nd = nd;
+            ra.prune = prune_enabled() ? 1 : 0;
+            std::memcpy(ra.need, dpl->need, sizeof(ra.need));
+            ra.base = base;
+            ra.stride = row_stride;
+            ra.stripe_stride = stripe_stride;
+            ra.nstripes = (int)nstripes;
+            ra.src_idx = dpl->src_idx;
+            ra.dst_idx = dpl->dst_idx;
+            HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
+            HIP_TRY(hipEventRecord(dpl->used, s));
+        }
+        if (!stream) HIP_TRY(hipStreamSynchronize(s));  // no caller stream: complete on return
+        return RS_OK;
+    }
+    // multi-pass codecs (n > 256): stripe by stripe
+    std::vector<uint8_t *> rows(c->total);
+    for (size_t z = 0; z < nstripes; z++) {
+        for (int i = 0; i < c->total; i++) rows[i] = base + z * stripe_stride + (uint64_t)i * row_stride;
+        if (int e = reconstruct_device(c, rows.data(), pr, S, recover_all != 0, s)) return e;
+    }
+    return RS_OK;
+}
+
 int rs_reconstruct_dev(rs_codec *c, uint8_t *const *d, const uint8_t *present, size_t S, int recover_all,
                        void *stream) {
     if (!c || !d || !present) return RS_ERR_INVALID_ARG;

@@ -1538,16 +1538,18 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     const int *outrow = nullptr;  // output index from the revealed-row mask (RevealIndex)
 #endif
     const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
+    uint8_t *const sbase = a.base ? a.base + (uint64_t)blockIdx.y * a.stripe_stride : nullptr;  // this stripe
     // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0
     struct ScaleIn {
         const RecArgs &a;
         uint64_t tile;
+        uint8_t *sbase;
         __device__ V operator()(int r, int u) const {
             V v = F::zero();
             const uint8_t *src;
-            if (a.base) {
+            if (sbase) {
                 const int i = a.src_idx[r];
-                src = i >= 0 ? a.base + (uint64_t)i * a.stride : nullptr;
+                src = i >= 0 ? sbase + (uint64_t)i * a.stride : nullptr;
             } else {
                 src = a.src[r];
             }
@@ -1560,6 +1562,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         const RecArgs &a;
         const int *outrow;
         uint64_t tile;
+        uint8_t *sbase;
         Need nw;
         __device__ void operator()(int r, int u, const V &x) const {
 #if RS_REC_LDS_OUTROW
@@ -1570,13 +1573,13 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
             if (j < 0 || !L::valid(tile, a.S, u)) return;
             V v = F::zero();
             F::mul_add(v, x, a.tw_out + (uint64_t)j * F::TWD);
-            uint8_t *dst = a.base ? a.base + (uint64_t)a.dst_idx[j] * a.stride : a.dst[j];
+            uint8_t *dst = sbase ? sbase + (uint64_t)a.dst_idx[j] * a.stride : a.dst[j];
             F::store(dst + tile, u, v);
         }
     };
     const LdsIO<FT> lio{lds};
-    lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile}, lio);
-    const Reveal rv{a, outrow, tile, load_need(a.need)};
+    lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
+    const Reveal rv{a, outrow, tile, sbase, load_need(a.need)};
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
     if constexpr (LOGN >= 3 && !RS_REC_UNFUSED_DERIV) {
         // fused with the FFT's first pass (radix-4 at dist D = N/4, one group,
@@ -2063,9 +2066,16 @@ bool r16_pick(uint64_t groups) {
 
 template <class F, class FT, int LOGN>
 hipError_t rec_lds_t(const RecArgs &a, hipStream_t s) {
-    const dim3 grid((unsigned)((a.S + LTile<F>::TB - 1) / LTile<F>::TB));
-    hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), grid, dim3(256), 0, s, a);
-    return hipGetLastError();
+    const unsigned gx = (unsigned)((a.S + LTile<F>::TB - 1) / LTile<F>::TB);
+    if (!a.base || a.nstripes <= 1) {
+        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), dim3(gx), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+    return for_y(a.nstripes, [&](int y0, int ny) {  // batched strided stripes: grid.y = stripe
+        RecArgs b = a;
+        b.base = a.base + (uint64_t)y0 * a.stripe_stride;
+        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), dim3(gx, (unsigned)ny), dim3(256), 0, s, b);
+    });
 }
 template <class F, class FT = F>
 hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
@@ -2260,13 +2270,14 @@ hipError_t rec_lds_w(int bits, int logn, bool sub, const RecArgs &a, hipStream_t
     return sub ? rec_lds_f<F16<W>, F16S<W>>(logn, a, s) : rec_lds_f<F16<W>>(logn, a, s);
 }
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s) {
-    if (bits == 16 && logn == 8 && !a.base && r16_pick((a.S + R16::TB - 1) / R16::TB)) {
+    if (bits == 16 && logn == 8 && !a.base && a.nstripes <= 1 && r16_pick((a.S + R16::TB - 1) / R16::TB)) {
         const dim3 grid((unsigned)((a.S + R16::TB - 1) / R16::TB));
         if (sub) hipLaunchKernelGGL((k_rec_r16<F16S<2>>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_rec_r16<F16<2>>), grid, dim3(256), 0, s, a);
         return hipGetLastError();
     }
-    const bool narrow = pick_narrow((a.S + 127) / 128 < kLdsMinGrid);
+    const uint64_t ns = a.base && a.nstripes > 1 ? (uint64_t)a.nstripes : 1;
+    const bool narrow = pick_narrow((a.S + 127) / 128 * ns < kLdsMinGrid);
     return narrow ? rec_lds_w<2>(bits, logn, sub, a, s) : rec_lds_w<4>(bits, logn, sub, a, s);
 }
 

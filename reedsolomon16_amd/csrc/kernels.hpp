@@ -14,6 +14,9 @@ struct RowSet {
     uint8_t *const *table;  // device array (nullable)
     uint8_t *base;
     uint64_t stride;
+    // strided only: nstripes stripes at base + y * stripe_stride (grid.y), one erasure pattern
+    uint64_t stripe_stride;
+    int nstripes;
 };
 
 // Fused register-resident encode (m <= 32): one lane owns a column unit of
@@ -73,6 +76,9 @@ struct RecArgs {
     // output j is shard dst_idx[j]; src / dst are then unused
     uint8_t *base;
     uint64_t stride;
+    // strided only: nstripes stripes at base + y * stripe_stride (grid.y), one erasure pattern
+    uint64_t stripe_stride;
+    int nstripes;
     const int *src_idx, *dst_idx;
     const int *pos;             // work row of each output
     const uint32_t *tw_in;      // n tables: errLocs scalings (mulgf16 semantics)

@@ -23,6 +23,8 @@ CONFIGS = {
     # stripe's kernel time is not hidden behind the per-call host cost
     "C2x16": (8, 10, 4, 1 << 20, "encode", 16),
     "C3x16": (16, 128, 32, 1 << 20, "encode", 16),
+    # one erasure pattern over 16 stripes in one launch (rs_reconstruct_dev_batch)
+    "C4x16": (16, 128, 32, 1 << 20, "reconstruct", 16),
 }
 # Host-resident (PCIe-inclusive) variants: shards in host memory, rs_encode /
 # rs_reconstruct stream them through the GPU.  "p" = pinned rows (rs_host_alloc).
@@ -137,6 +139,8 @@ def main():
                 c.encode_dev_batch(slab, st)
             elif op == "verify":
                 c.verify_dev(rows, st)
+            elif ns > 1:
+                c.reconstruct_dev_batch(slab, present, stream=st)
             else:
                 c.reconstruct_dev(rows, present, stream=st)
 

@@ -511,6 +511,43 @@ def test_host_reconstruct_into_capacity():
     assert np.array_equal(work[er[0]], full[er[0]]) and not np.any(small)
 
 
+# Batched device reconstruct (rs_reconstruct_dev_batch): one erasure pattern
+# over many stripes in one launch, rows at a padded stride and stripes at a
+# padded stripe stride; n <= 256 codecs run the LDS kernel with grid.y =
+# stripe, n > 256 codecs go stripe by stripe.  Rebuilt bytes must equal the
+# encoded stripes (data and parity erasures), and ReconstructData must leave
+# erased parity rows untouched.
+@pytest.mark.parametrize("bits,k,p,S,ns", [(16, 128, 32, 1 << 16, 5), (8, 10, 4, 1 << 14, 7), (16, 300, 100, 4096, 3),
+                                           (16, 20, 10, 2048, 1)])
+def test_reconstruct_dev_batch(torch_dev, bits, k, p, S, ns):
+    torch = torch_dev
+    RS, total = S + 3072, k + p
+    SS = total * RS + 4096
+    buf = torch.zeros(ns * SS, dtype=torch.uint8, device="cuda")
+    slab = buf.as_strided((ns, total, S), (SS, RS, 1))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(k + p + ns)
+    slab[:, :k] = torch.randint(0, 256, (ns, k, S), dtype=torch.uint8, device="cuda", generator=g)
+    c = rs.ReedSolomon(k, p, bits)
+    c.encode_dev_batch(slab)
+    torch.cuda.synchronize()
+    full = slab.clone()
+    rng = np.random.default_rng(k + p + S)
+    er = rng.choice(total, p, replace=False)
+    present = np.ones(total, bool)
+    present[er] = False
+    for recover_all in (True, False):
+        slab[:, torch.from_numpy(er).cuda()] = 0
+        c.reconstruct_dev_batch(slab, present, recover_all)
+        torch.cuda.synchronize()
+        for z in range(ns):
+            for i in range(total):
+                if i < k or recover_all:
+                    assert torch.equal(slab[z, i], full[z, i]), (recover_all, z, i)
+                elif not present[i]:
+                    assert not torch.any(slab[z, i]), (z, i)
+
+
 # Codec scratch shared across caller streams: device-resident encodes return
 # before their kernels finish, so a second call on another stream must not
 # overwrite the row-pointer table (non-strided rows) or the multi-pass work
