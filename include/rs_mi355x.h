@@ -172,6 +172,11 @@ int rs_reconstruct_dev_batch(rs_codec *codec, uint8_t *base, size_t row_stride, 
  * Asynchronous on `stream`. */
 int rs_encode_dev_batch(rs_codec *codec, uint8_t *d_base, size_t row_stride, size_t stripe_stride,
                         int nstripes, size_t shard_size, void *stream);
+/* Verify (leopard16.go:361-387) of nstripes strided stripes in one launch
+ * (rs_encode_dev_batch's layout): *ok = 1 when every stripe's parity matches
+ * its data, 0 when any stripe differs.  Synchronous (the flag is read back). */
+int rs_verify_dev_batch(rs_codec *codec, uint8_t *d_base, size_t row_stride, size_t stripe_stride, int nstripes,
+                        size_t shard_size, int *ok, void *stream);
 
 /* Name of the kernel path the codec uses for encode ("reg-m32", "lds", "multipass", ...). */
 const char *rs_encode_path(const rs_codec *codec);

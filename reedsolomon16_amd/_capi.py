@@ -41,6 +41,7 @@ def lib() -> C.CDLL:
     L.rs_verify_dev.argtypes = [vp, P(vp), sz, P(i32), vp]
     L.rs_reconstruct_dev.argtypes = [vp, P(vp), P(C.c_uint8), sz, i32, vp]
     L.rs_reconstruct_dev_batch.argtypes = [vp, vp, sz, sz, sz, P(C.c_uint8), sz, i32, vp]
+    L.rs_verify_dev_batch.argtypes = [vp, vp, sz, sz, i32, sz, P(i32), vp]
     L.rs_encode_dev_batch.argtypes = [vp, vp, sz, sz, i32, sz, vp]
     L.rs_set_host_segment.argtypes = [vp, sz]
     L.rs_split_shard_size.argtypes = [vp, sz, P(sz)]

@@ -434,6 +434,19 @@ class ReedSolomon:
         pr = (C.c_uint8 * self.total_shards())(*[1 if x else 0 for x in present])
         _check(self._L.rs_reconstruct_dev(self._h, ptrs, pr, S, int(recover_all), _stream_handle(stream)))
 
+    def verify_dev_batch(self, slab, stream=None) -> bool:
+        """Verify every stripe of a [nstripes, k+p, S] uint8 CUDA tensor in one
+        launch (rs_verify_dev_batch): True when all stripes verify."""
+        if slab.dim() != 3 or slab.shape[1] != self.total_shards():
+            raise TypeError("slab must be a [nstripes, k+p, S] uint8 CUDA tensor")
+        if not slab.is_cuda or slab.dtype.itemsize != 1 or slab.stride(2) != 1:
+            raise TypeError("slab rows must be contiguous uint8 on a CUDA device")
+        n, _, S = slab.shape
+        ok = C.c_int(0)
+        _check(self._L.rs_verify_dev_batch(self._h, slab.data_ptr(), slab.stride(1), slab.stride(0), n, S, C.byref(ok),
+                                           _stream_handle(stream)))
+        return bool(ok.value)
+
     def reconstruct_dev_batch(self, slab, present: Sequence[bool], recover_all: bool = True, stream=None) -> None:
         """Rebuild the missing shards of every stripe of a [nstripes, k+p, S]
         uint8 CUDA tensor in place, all with the same erasure pattern

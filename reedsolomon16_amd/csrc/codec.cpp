@@ -1390,6 +1390,30 @@ int rs_verify_dev(rs_codec *c, uint8_t *const *d, size_t S, int *ok, void *strea
     return RS_OK;
 }
 
+int rs_verify_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size_t stripe_stride, int nstripes, size_t S,
+                        int *ok, void *stream) {
+    if (!c || !base || !ok || nstripes <= 0) return RS_ERR_INVALID_ARG;
+    *ok = 0;
+    if (S == 0) return RS_ERR_SHARD_NO_DATA;
+    if (S % 64) return RS_ERR_INVALID_SHARD_SIZE;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (int ie = ensure_device(c)) return ie;
+    hipStream_t s = pick_stream(c, stream);
+    RowSet data{nullptr, base, row_stride}, par{nullptr, base + (size_t)c->k * row_stride, row_stride};
+    int e = scratch_acquire(c, s);
+    if (e) return e;
+    HIP_TRY(hipMemsetAsync(c->dflag, 0, sizeof(int), s));
+    e = encode_device(c, data, par, S, stripe_stride, nstripes, c->dflag, s);
+    if (e) return e;
+    e = scratch_release(c, s);
+    if (e) return e;
+    HIP_TRY(hipMemcpyAsync(c->hflag, c->dflag, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *ok = *(volatile int *)c->hflag == 0;
+    return RS_OK;
+}
+
 int rs_reconstruct_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size_t stripe_stride, size_t nstripes,
                              const uint8_t *present, size_t S, int recover_all, void *stream) {
     if (!c || !base || !present || nstripes == 0 || nstripes > (size_t)INT32_MAX) return RS_ERR_INVALID_ARG;

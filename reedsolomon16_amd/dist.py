@@ -101,3 +101,13 @@ def encode_sharded_batch(slab, rank: int, world: int, codec, stream=None) -> Non
     loc = local_stripes(slab, rank, world)
     if loc.shape[2]:
         codec.encode_dev_batch(loc, stream)
+
+
+def reconstruct_sharded_batch(slab, present: Sequence[bool], rank: int, world: int, codec, recover_all: bool = True,
+                              stream=None) -> None:
+    """Rebuild this rank's byte range of the missing shards of n stripes with
+    one erasure pattern (a lost device) in one launch (rs_reconstruct_dev_batch
+    over the strided view; no collective: every rank holds the same pattern)."""
+    loc = local_stripes(slab, rank, world)
+    if loc.shape[2]:
+        codec.reconstruct_dev_batch(loc, present, recover_all, stream)

@@ -25,6 +25,7 @@ CONFIGS = {
     "C3x16": (16, 128, 32, 1 << 20, "encode", 16),
     # one erasure pattern over 16 stripes in one launch (rs_reconstruct_dev_batch)
     "C4x16": (16, 128, 32, 1 << 20, "reconstruct", 16),
+    "C3vx16": (16, 128, 32, 1 << 20, "verify", 16),
 }
 # Host-resident (PCIe-inclusive) variants: shards in host memory, rs_encode /
 # rs_reconstruct stream them through the GPU.  "p" = pinned rows (rs_host_alloc).
@@ -138,7 +139,7 @@ def main():
             if op == "encode":
                 c.encode_dev_batch(slab, st)
             elif op == "verify":
-                c.verify_dev(rows, st)
+                c.verify_dev_batch(slab, st) if ns > 1 else c.verify_dev(rows, st)
             elif ns > 1:
                 c.reconstruct_dev_batch(slab, present, stream=st)
             else:

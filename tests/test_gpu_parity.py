@@ -548,6 +548,55 @@ def test_reconstruct_dev_batch(torch_dev, bits, k, p, S, ns):
                     assert not torch.any(slab[z, i]), (z, i)
 
 
+def test_reconstruct_sharded_batch_world8(torch_dev):
+    """dist.reconstruct_sharded_batch: 8 byte-range slices of the same stripes,
+    each rebuilt in one launch on its own, reassemble the encoded stripes."""
+    from reedsolomon16_amd import dist as rsd
+    torch = torch_dev
+    k, p, S, ns, world = 128, 32, 1 << 15, 3, 8
+    g = torch.Generator(device="cuda")
+    g.manual_seed(88)
+    slab = torch.zeros((ns, k + p, S), dtype=torch.uint8, device="cuda")
+    slab[:, :k] = torch.randint(0, 256, (ns, k, S), dtype=torch.uint8, device="cuda", generator=g)
+    c = rs.New16(k, p)
+    c.encode_dev_batch(slab)
+    torch.cuda.synchronize()
+    full = slab.clone()
+    er = np.random.default_rng(88).choice(k + p, p, replace=False)
+    present = np.ones(k + p, bool)
+    present[er] = False
+    slab[:, torch.from_numpy(er).cuda()] = 0
+    for r in range(world):
+        rsd.reconstruct_sharded_batch(slab, present, r, world, c)
+    torch.cuda.synchronize()
+    assert torch.equal(slab, full)
+
+
+@pytest.mark.parametrize("bits,k,p,S,ns", [(16, 128, 32, 1 << 16, 6), (8, 10, 4, 1 << 14, 5), (16, 1024, 256, 4096, 2)])
+def test_verify_dev_batch(torch_dev, bits, k, p, S, ns):
+    """rs_verify_dev_batch: all stripes clean -> True; one flipped byte in any
+    one stripe (data or parity row) -> False; restored -> True."""
+    torch = torch_dev
+    RS = S + 3072
+    SS = (k + p) * RS
+    buf = torch.zeros(ns * SS, dtype=torch.uint8, device="cuda")
+    slab = buf.as_strided((ns, k + p, S), (SS, RS, 1))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(k + ns)
+    slab[:, :k] = torch.randint(0, 256, (ns, k, S), dtype=torch.uint8, device="cuda", generator=g)
+    c = rs.ReedSolomon(k, p, bits)
+    c.encode_dev_batch(slab)
+    assert c.verify_dev_batch(slab)
+    rng = np.random.default_rng(ns)
+    for z, row in ((ns - 1, 0), (0, k + p - 1), (ns // 2, k)):
+        col = int(rng.integers(0, S))
+        old = slab[z, row, col].item()
+        slab[z, row, col] = old ^ 0x10
+        assert not c.verify_dev_batch(slab), (z, row, col)
+        slab[z, row, col] = old
+        assert c.verify_dev_batch(slab)
+
+
 # Codec scratch shared across caller streams: device-resident encodes return
 # before their kernels finish, so a second call on another stream must not
 # overwrite the row-pointer table (non-strided rows) or the multi-pass work
