@@ -231,12 +231,16 @@ __device__ __forceinline__ void hp_get(uint32_t lbase, int row, Half &v) {
 // Cache-policy bits of the data-row loads and parity stores (buffer
 // instruction aux: 1 = sc0, 2 = nt, 16 = sc1; MI355X_MICROARCH.md stores
 // table).  0 = default policy; other values are A/B experiments.
+#ifndef RS_BS_VERIFY_DMA
+#define RS_BS_VERIFY_DMA 0  // 1: verify stages the parity through LDS by DMA during the last FFT layers (measured slower)
+#endif
 #ifndef RS_BS_LOAD_AUX
 #define RS_BS_LOAD_AUX 0
 #endif
 #ifndef RS_BS_STORE_AUX
 #define RS_BS_STORE_AUX 0
 #endif
+typedef __attribute__((address_space(3))) void lds_void_t;
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int LOGM, bool VERIFY>
@@ -432,6 +436,30 @@ struct HpEncoder {
             lds_barrier();
 #pragma unroll
             for (int j = 0; j < RW; j++) hp_get(lbase, RW * w + j, R[j]);
+            if constexpr (VERIFY && RS_BS_VERIFY_DMA) {
+                // The image is free once every wave has read its rows: the
+                // parity rows this lane will compare come into it by LDS-DMA
+                // (lane-for-lane the compare's own addressing, one KB-slot per
+                // (row, piece) of the wave) while fft_b and the transposes run.
+                lds_barrier();
+                const __amdgpu_buffer_rsrc_t vps = __builtin_amdgcn_make_buffer_rsrc(
+                    (void *)(a.parity + (uint64_t)cur.stripe * a.stripe_stride), 0, (int)a.pspan, 0x00020000);
+#ifdef RS_HP_ABL_COALESCED
+                const uint32_t vvoff = (uint32_t)cur.ct * TILE + (uint32_t)blk * 16 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
+                constexpr uint32_t VQS = 512;
+#else
+                const uint32_t vvoff = (uint32_t)cur.ct * TILE + (uint32_t)blk * 64 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
+                constexpr uint32_t VQS = 16;
+#endif
+                const uint32_t l0 = __builtin_amdgcn_readfirstlane(lbase);
+#pragma unroll
+                for (int i = 0; i < HR; i++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            vps, (lds_void_t *)(uintptr_t)(l0 + (uint32_t)(((w * HR + i) * 4 + k) * 1024)), 16,
+                            vvoff + k * VQS, (uint32_t)(RW * w + i) * (uint32_t)a.row_stride, 0, 0);
+            }
             dispatch<4>(w, [&](auto W) { fft_b<decltype(W)::value>(); });
             hp_swap_halves<HR>(R);
             // parity rows RW*w + HR*h + i < p, through a descriptor over the
@@ -448,6 +476,7 @@ struct HpEncoder {
 #endif
             asm volatile("" : "+v"(voff));
             uint32_t bad = 0;
+            if constexpr (VERIFY && RS_BS_VERIFY_DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the parity DMA has landed
             if (col < a.S) {
 #pragma unroll
                 for (int i = 0; i < HR; i++) {
@@ -467,7 +496,13 @@ struct HpEncoder {
                         const u32x4 v = k < 2 ? u32x4{R[i][o], R[i][o + 1], R[i][o + 2], R[i][o + 3]}
                                               : u32x4{R[HR + i][o], R[HR + i][o + 1], R[HR + i][o + 2], R[HR + i][o + 3]};
                         if constexpr (VERIFY) {
+#if RS_BS_VERIFY_DMA
+                            (void)soff;
+                            const u32x4 old = *(const __attribute__((address_space(3))) u32x4 *)(uintptr_t)(
+                                lbase + (uint32_t)(((w * HR + i) * 4 + k) * 1024));
+#else
                             const u32x4 old = __builtin_amdgcn_raw_buffer_load_b128(ps, voff + k * QS, soff, 0);
+#endif
                             bad |= (old[0] ^ v[0]) | (old[1] ^ v[1]) | (old[2] ^ v[2]) | (old[3] ^ v[3]);
                         } else {
 #if defined(RS_BS_ABL_NOSTORE)
@@ -482,7 +517,10 @@ struct HpEncoder {
             if constexpr (VERIFY) {
                 // one store per wave, not per lane
                 const uint64_t m = __ballot(bad != 0);
-                if (m && lane == __ffsll((unsigned long long)m) - 1)
+                // a set flag stays set: skip the store (a failing verify would
+                // otherwise store once per wave per tile into one contended word)
+                if (m && lane == __ffsll((unsigned long long)m) - 1 &&
+                    __hip_atomic_load(a.mismatch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
                     __hip_atomic_store(a.mismatch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             cur = nxt;

@@ -125,7 +125,8 @@ __device__ __forceinline__ void ldw_lds(const uint8_t *p, uint32_t (&v)[W]) {
 // suffices.  One lane per wave stores.
 __device__ __forceinline__ void flag_mismatch(int *f, bool bad) {
     const uint64_t m = __ballot(bad);
-    if (m && __lane_id() == (unsigned)(__ffsll((unsigned long long)m) - 1))
+    if (m && __lane_id() == (unsigned)(__ffsll((unsigned long long)m) - 1) &&
+        __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)  // set stays set: no contended store
         __hip_atomic_store(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

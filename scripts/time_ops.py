@@ -26,6 +26,8 @@ CONFIGS = {
     # one erasure pattern over 16 stripes in one launch (rs_reconstruct_dev_batch)
     "C4x16": (16, 128, 32, 1 << 20, "reconstruct", 16),
     "C3vx16": (16, 128, 32, 1 << 20, "verify", 16),
+    # failing verify (every stripe corrupt): the flag path
+    "C3vbadx16": (16, 128, 32, 1 << 20, "verify_bad", 16),
 }
 # Host-resident (PCIe-inclusive) variants: shards in host memory, rs_encode /
 # rs_reconstruct stream them through the GPU.  "p" = pinned rows (rs_host_alloc).
@@ -129,6 +131,10 @@ def main():
         ne = CONFIGS[name][6] if len(CONFIGS[name]) > 6 else p
         c = rs.ReedSolomon(k, p, bits)
         slab = torch.randint(0, 256, (ns, k + p, S), dtype=torch.uint8, device="cuda")
+        if op == "verify":  # the passing case; verify_bad times random (failing) stripes
+            c.encode_dev_batch(slab)
+        if op == "verify_bad":
+            op = "verify"
         rows = slab[0]
         present = np.ones(k + p, bool)
         present[np.random.default_rng(0x5EED).choice(k + p, ne, replace=False)] = False
