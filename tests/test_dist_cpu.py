@@ -94,7 +94,33 @@ def _worker(rank, world, port, bits, k, p, S, q):
     broken[er] = 0
     rsd.reconstruct_sharded(broken, present, rank, world, rec)
     rec_ok = bool(np.array_equal(broken[:, lo:hi], rows[:, lo:hi]))
-    q.put((rank, good, ok_all, bad_all, rec_ok))
+
+    # batched layout: 2 stripes in one [n, k+p, S] slab, each rank's column
+    # slice handed to the codec's batch entry points (a CPU stand-in here)
+    class _CpuBatch:
+        def encode_dev_batch(self, loc, stream=None):
+            for z in range(loc.shape[0]):
+                enc(loc[z].numpy())
+
+        def reconstruct_dev_batch(self, loc, present, recover_all=True, stream=None):
+            for z in range(loc.shape[0]):
+                rec(loc[z].numpy(), present)
+
+    datas = [np.random.default_rng(500 + z).integers(0, 256, (k, S), dtype=np.uint8) for z in range(2)]
+    slab = torch.zeros((2, k + p, S), dtype=torch.uint8)
+    for z in range(2):
+        slab[z, :k] = torch.from_numpy(datas[z])
+    rsd.encode_sharded_batch(slab, rank, world, _CpuBatch())
+    refs = [orc.encode(bits, k, p, datas[z]) for z in range(2)]
+    benc_ok = all(np.array_equal(slab[z, k:, lo:hi].numpy(), refs[z][:, lo:hi]) for z in range(2))
+    full_b = slab.clone()
+    for z in range(2):
+        full_b[z, k:] = torch.from_numpy(refs[z])
+    broken_b = full_b.clone()
+    broken_b[:, torch.from_numpy(er)] = 0
+    rsd.reconstruct_sharded_batch(broken_b, present, rank, world, _CpuBatch())
+    brec_ok = bool(torch.equal(broken_b[:, :, lo:hi], full_b[:, :, lo:hi]))
+    q.put((rank, good, ok_all, bad_all, rec_ok and benc_ok and brec_ok))
     dist.destroy_process_group()
 
 
