@@ -10,7 +10,12 @@ the persistent grid's fill and drain: on one box the 8-rank byte-range slice
 roofline for 64 / 128 / 256 stripes per launch, full rows at 0.61 / 0.61-0.62
 / 0.63-0.64 for 32 / 128 / 256 (profiles/r02_batch_slice.txt).
 
-Multi-GPU (one process per GPU, launched by torch.distributed.run):
+Multi-GPU (one process per GPU).  Under torch.distributed.run (WORLD_SIZE set)
+every rank checks WORLD_SIZE == --gpus.  Started directly with --gpus N > 1,
+the parent launches `python -m torch.distributed.run --nproc-per-node N` on
+this same command line before it imports torch or touches a GPU, and exits
+with the child's return code.  --dry-run runs the rank layout with gloo on the
+CPU (no GPU): each rank reports its byte range.
   --split bytes   (default) the north-star layout: rank r owns the byte range
                   dist.byte_range(S, r, N) of every shard of the same B stripes
                   (column independence, leopard16.go:778-792) and encodes it;
@@ -105,6 +110,47 @@ def load_traffic(kernel_name: str, workload: str, stripes: int):
         return None
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Start n ranks of this command under torch.distributed.run (a child
+    process: nothing in this process has touched the GPU) and return its rc."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, rank: int, world: int) -> None:
+    """The rank layout without a GPU: gloo process group, each rank's byte
+    range of the workload's shards, gathered on rank 0 and printed as JSON."""
+    import torch.distributed as dist
+
+    from reedsolomon16_amd import dist as rsd
+
+    if "WORLD_SIZE" in os.environ:
+        dist.init_process_group("gloo")
+    else:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
+    K, P, S = WORKLOADS[args.workload]
+    lo, hi = rsd.byte_range(S, rank, world) if args.split == "bytes" else (0, S)
+    got = [None] * world
+    dist.all_gather_object(got, {"rank": rank, "byte_range": [lo, hi], "world": dist.get_world_size()})
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_requested": args.gpus, "workload": args.workload,
+                          "split": args.split, "ranks": got}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -122,7 +168,19 @@ def main():
                     help="bytes between consecutive resident rows (HBM layout: row stride = row bytes + pad; "
                          "64-byte multiple); the unpadded layout is timed too and reported beside it")
     ap.add_argument("--no-unpadded", action="store_true", help="skip timing the unpadded layout")
+    ap.add_argument("--dry-run", action="store_true", help="rank layout only: gloo on the CPU, no GPU")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # before any GPU call in this process
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return
 
     import torch
     import torch.distributed as dist
@@ -130,9 +188,6 @@ def main():
     import reedsolomon16_amd as rs
     from reedsolomon16_amd import dist as rsd
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -199,7 +254,11 @@ def main():
         _, one_ms = timed(slab[:1], max(50, args.steps))
 
     t = torch.tensor([el, kern_ms, one_ms or 0.0, flat_ms or 0.0], dtype=torch.float64, device=dev)
+    per_rank = [kern_ms]
     if world > 1:
+        allk = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(allk, t[1:2].clone())
+        per_rank = [float(x) for x in allk]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el, kern_ms, one_ms, flat_ms = float(t[0]), float(t[1]), float(t[2]) or None, float(t[3]) or None
 
@@ -239,7 +298,9 @@ def main():
                 "layout": f"rows at a stride of {W} + {pad} bytes, stripes back to back",
             },
             "hbm_gib_s": round(world * args.steps * alg_bytes / el / 2**30, 2),
-            "per_rank_kernel_ms": round(kern_ms, 5),
+            "per_rank_kernel_ms": [round(x, 5) for x in per_rank],
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() if world > 1 else None,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),

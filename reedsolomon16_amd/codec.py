@@ -388,10 +388,14 @@ class ReedSolomon:
         ptrs = (C.c_void_p * k)()
         lens = (C.c_size_t * k)()
         keep = []
+        empty = np.zeros(1, dtype=np.uint8)  # a non-nil zero-length shard (Go: counts 0 bytes, leopard16.go:239-250)
         for i in range(k):
             s = shards[i]
-            if s is None or len(s) == 0:
+            if s is None:  # nil: ErrReconstructRequired
                 ptrs[i], lens[i] = None, 0
+                continue
+            if len(s) == 0:
+                ptrs[i], lens[i] = empty.ctypes.data, 0
                 continue
             a = np.ascontiguousarray(s, dtype=np.uint8)
             keep.append(a)

@@ -228,19 +228,6 @@ __device__ __forceinline__ void hp_get(uint32_t lbase, int row, Half &v) {
 // release/acquire fence, which waits for every outstanding global load
 // (vmcnt(0)) and so would drain the next chunk's prefetch at the first
 // barrier of every chunk; this waits for LDS traffic alone.
-// Cache-policy bits of the data-row loads and parity stores (buffer
-// instruction aux: 1 = sc0, 2 = nt, 16 = sc1; MI355X_MICROARCH.md stores
-// table).  0 = default policy; other values are A/B experiments.
-#ifndef RS_BS_VERIFY_DMA
-#define RS_BS_VERIFY_DMA 0  // 1: verify stages the parity through LDS by DMA during the last FFT layers (measured slower)
-#endif
-#ifndef RS_BS_LOAD_AUX
-#define RS_BS_LOAD_AUX 0
-#endif
-#ifndef RS_BS_STORE_AUX
-#define RS_BS_STORE_AUX 0
-#endif
-typedef __attribute__((address_space(3))) void lds_void_t;
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int LOGM, bool VERIFY>
@@ -293,13 +280,8 @@ struct HpEncoder {
             (void *)(a.data + (L.live ? (uint64_t)L.stripe * a.stripe_stride : 0)), 0, (int)range, 0x00020000);
         // lane part of the offset (block, half); opaque so that the compiler
         // does not precompute every chunk's offsets
-#ifdef RS_HP_ABL_COALESCED  // ablation: same bytes, lane-contiguous 16-byte pieces (wrong layout)
-        uint32_t voff = (uint32_t)L.ct * TILE + (uint32_t)blk * 16 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
-        constexpr uint32_t QS = 512;
-#else
         uint32_t voff = (uint32_t)L.ct * TILE + (uint32_t)blk * 64 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
         constexpr uint32_t QS = 16;
-#endif
         asm volatile("" : "+v"(voff));
 #pragma unroll
         for (int i = I0; i < I1; i++) {
@@ -307,7 +289,7 @@ struct HpEncoder {
             const uint32_t soff = (uint32_t)(M * c + RW * w + i) * (uint32_t)a.row_stride;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * QS, soff, RS_BS_LOAD_AUX);
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * QS, soff, 0);
                 uint32_t *d = q < 2 ? &St[i][q * 4] : &St[HR + i][(q - 2) * 4];
                 d[0] = x[0], d[1] = x[1], d[2] = x[2], d[3] = x[3];
             }
@@ -436,30 +418,6 @@ struct HpEncoder {
             lds_barrier();
 #pragma unroll
             for (int j = 0; j < RW; j++) hp_get(lbase, RW * w + j, R[j]);
-            if constexpr (VERIFY && RS_BS_VERIFY_DMA) {
-                // The image is free once every wave has read its rows: the
-                // parity rows this lane will compare come into it by LDS-DMA
-                // (lane-for-lane the compare's own addressing, one KB-slot per
-                // (row, piece) of the wave) while fft_b and the transposes run.
-                lds_barrier();
-                const __amdgpu_buffer_rsrc_t vps = __builtin_amdgcn_make_buffer_rsrc(
-                    (void *)(a.parity + (uint64_t)cur.stripe * a.stripe_stride), 0, (int)a.pspan, 0x00020000);
-#ifdef RS_HP_ABL_COALESCED
-                const uint32_t vvoff = (uint32_t)cur.ct * TILE + (uint32_t)blk * 16 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
-                constexpr uint32_t VQS = 512;
-#else
-                const uint32_t vvoff = (uint32_t)cur.ct * TILE + (uint32_t)blk * 64 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
-                constexpr uint32_t VQS = 16;
-#endif
-                const uint32_t l0 = __builtin_amdgcn_readfirstlane(lbase);
-#pragma unroll
-                for (int i = 0; i < HR; i++)
-#pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                            vps, (lds_void_t *)(uintptr_t)(l0 + (uint32_t)(((w * HR + i) * 4 + k) * 1024)), 16,
-                            vvoff + k * VQS, (uint32_t)(RW * w + i) * (uint32_t)a.row_stride, 0, 0);
-            }
             dispatch<4>(w, [&](auto W) { fft_b<decltype(W)::value>(); });
             hp_swap_halves<HR>(R);
             // parity rows RW*w + HR*h + i < p, through a descriptor over the
@@ -467,25 +425,15 @@ struct HpEncoder {
             const uint32_t col = (uint32_t)cur.ct * TILE + (uint32_t)blk * 64;
             const __amdgpu_buffer_rsrc_t ps = __builtin_amdgcn_make_buffer_rsrc(
                 (void *)(a.parity + (uint64_t)cur.stripe * a.stripe_stride), 0, (int)a.pspan, 0x00020000);
-#ifdef RS_HP_ABL_COALESCED
-            uint32_t voff = (uint32_t)cur.ct * TILE + (uint32_t)blk * 16 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
-            constexpr uint32_t QS = 512;
-#else
             uint32_t voff = col + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
             constexpr uint32_t QS = 16;
-#endif
             asm volatile("" : "+v"(voff));
             uint32_t bad = 0;
-            if constexpr (VERIFY && RS_BS_VERIFY_DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the parity DMA has landed
             if (col < a.S) {
 #pragma unroll
                 for (int i = 0; i < HR; i++) {
                     const int row = RW * w + HR * h + i;
-#ifdef RS_HP_ABL_FIXED_P  // ablation: parity count fixed at compile time
-                    if (row >= RS_HP_ABL_FIXED_P) continue;
-#else
                     if (row >= a.p) continue;
-#endif
                     hp_psi<TW>(R[i], R[HR + i]);
                     bs_transpose8(R[i]);
                     bs_transpose8(R[HR + i]);
@@ -496,19 +444,13 @@ struct HpEncoder {
                         const u32x4 v = k < 2 ? u32x4{R[i][o], R[i][o + 1], R[i][o + 2], R[i][o + 3]}
                                               : u32x4{R[HR + i][o], R[HR + i][o + 1], R[HR + i][o + 2], R[HR + i][o + 3]};
                         if constexpr (VERIFY) {
-#if RS_BS_VERIFY_DMA
-                            (void)soff;
-                            const u32x4 old = *(const __attribute__((address_space(3))) u32x4 *)(uintptr_t)(
-                                lbase + (uint32_t)(((w * HR + i) * 4 + k) * 1024));
-#else
                             const u32x4 old = __builtin_amdgcn_raw_buffer_load_b128(ps, voff + k * QS, soff, 0);
-#endif
                             bad |= (old[0] ^ v[0]) | (old[1] ^ v[1]) | (old[2] ^ v[2]) | (old[3] ^ v[3]);
                         } else {
 #if defined(RS_BS_ABL_NOSTORE)
                             asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
 #else
-                            __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * QS, soff, RS_BS_STORE_AUX);
+                            __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * QS, soff, 0);
 #endif
                         }
                     }
@@ -539,11 +481,7 @@ __global__ void __launch_bounds__(256, kHpWgPerCu<LOGM>) k_encode_hp(BsArgs a) {
     e.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     e.h = e.lane >> 5;
     e.blk = e.lane & 31;
-#ifdef RS_HP_ABL_FIXED_NCH  // ablation: chunk count fixed at compile time
-    e.nch = RS_HP_ABL_FIXED_NCH;
-#else
     e.nch = (a.k + (1 << LOGM) - 1) >> LOGM;
-#endif
     e.lbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)lds + e.lane * 16;
     e.run();
 }
@@ -583,12 +521,19 @@ bool encode_bs_available(int k, int p, const uint32_t *ifft_logs, const uint32_t
                            : hp_tables_match<4>(k, ifft_logs, fft_logs, mod);
 }
 
+bool encode_bs_fits(int k, int p, uint64_t row_stride, uint64_t S) {
+    if (k < 1 || p < 9 || p > 32) return false;
+    const int m = 1 << hp_logm(p);
+    const uint64_t rows = (uint64_t)(k + m - 1) / m * m;  // padding rows of the last chunk are loaded too
+    const uint64_t cols = (S + 2047) / 2048 * 2048;       // lanes of the last tile past the row end
+    return (rows - 1) * row_stride + cols < (1ull << 32);
+}
+
 hipError_t launch_encode_bs(bool verify, const BsArgs &a, int cus, hipStream_t s) {
     if (a.k < 1 || a.p < 9 || a.p > 32) return hipErrorNotSupported;
     const int logm = hp_logm(a.p);
     if ((a.k + (1 << logm) - 1) >> logm > (logm == 5 ? HpTab<5>::NCH : HpTab<4>::NCH)) return hipErrorNotSupported;
-    // buffer offsets are 32-bit: the rows of one stripe must span < 4 GiB
-    if ((uint64_t)(std::max(a.k, a.p) - 1) * a.row_stride + a.S >= (1ull << 32)) return hipErrorNotSupported;
+    if (!encode_bs_fits(a.k, a.p, a.row_stride, a.S)) return hipErrorNotSupported;
     return logm == 5 ? launch_hp_t<5>(verify, a, cus, s) : launch_hp_t<4>(verify, a, cus, s);
 }
 

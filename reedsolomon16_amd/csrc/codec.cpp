@@ -94,11 +94,23 @@ struct DevPlan {
     const int *pos = nullptr;
     const int *src_idx = nullptr, *dst_idx = nullptr;  // pl.src_shard / pl.dst_shard (strided launches)
     uint32_t need[8] = {};
-    hipEvent_t used = nullptr;  // recorded after every launch that reads blob
+    // One event per stream that launched with this plan, recorded after each
+    // such launch: an eviction frees blob only after the last launch on every
+    // one of those streams (one event alone would cover only the latest).
+    std::vector<std::pair<hipStream_t, hipEvent_t>> used;
+    hipError_t mark_used(hipStream_t s) {
+        for (auto &u : used)
+            if (u.first == s) return hipEventRecord(u.second, s);
+        hipEvent_t ev = nullptr;
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+        used.emplace_back(s, ev);
+        return hipEventRecord(ev, s);
+    }
     ~DevPlan() {
-        if (used) {
-            (void)hipEventSynchronize(used);
-            (void)hipEventDestroy(used);
+        for (auto &u : used) {
+            (void)hipEventSynchronize(u.second);
+            (void)hipEventDestroy(u.second);
         }
         blob.release();
     }
@@ -494,7 +506,7 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
         // bit-sliced kernel: strided rows, one row stride for data and parity
         const uint64_t span = (uint64_t)(c->k - 1) * data.stride + S;
         if (c->bs_ok && !data.table && !par.table && data.stride == par.stride && data.stride >= S &&
-            (uint64_t)(std::max(c->k, c->p) - 1) * data.stride + S < (1ull << 32)) {
+            encode_bs_fits(c->k, c->p, data.stride, S)) {
             BsArgs b{};
             b.data = data.base;
             b.parity = par.base;
@@ -682,7 +694,6 @@ int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipS
         ra.tw_fft = c->dtw_fft.p;
         ra.S = S;
         ra.mtrunc = c->m + c->k;
-    ra.m = c->m;
         ra.m = c->m;
         ra.nd = nd;
         ra.prune = prune_enabled() ? 1 : 0;
@@ -735,7 +746,6 @@ int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
     dp->src_idx = (const int *)(dp->blob.p + o_si);
     dp->dst_idx = (const int *)(dp->blob.p + o_di);
     for (int p : pl.pos) dp->need[p >> 5] |= 1u << (p & 31);
-    HIP_TRY(hipEventCreateWithFlags(&dp->used, hipEventDisableTiming));
     c->dplan_cache.emplace_front(std::move(key), std::move(dp));
     if (c->dplan_cache.size() > 16) c->dplan_cache.pop_back();  // waits for the plan's last launch
     *out = c->dplan_cache.front().second.get();
@@ -787,7 +797,7 @@ int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uin
             ra.src_idx = dp->src_idx;
             ra.dst_idx = dp->dst_idx;
             HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
-            HIP_TRY(hipEventRecord(dp->used, s));
+            HIP_TRY(dp->mark_used(s));
             return RS_OK;
         }
     }
@@ -818,7 +828,7 @@ int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uin
     HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
     HIP_TRY(hipEventRecord(c->ring_ev[i], s));
     c->ring_used[i] = true;
-    HIP_TRY(hipEventRecord(dp->used, s));
+    HIP_TRY(dp->mark_used(s));
     return RS_OK;
 }
 
@@ -1013,14 +1023,21 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     }
     const uint64_t seg = host_segment(c, S, in_rows.size());
     const uint64_t slab = (uint64_t)total * seg;
-    if (c->stage.n < (size_t)kHostBufs * slab) {  // a reallocation waits for queued segments
+    const uint64_t slab_al = (slab + 255) / 256 * 256;
+    if (c->stage.n / kHostBufs < slab_al) {  // a reallocation waits for queued segments
         HIP_TRY(hipStreamSynchronize(c->s_in));
         HIP_TRY(hipStreamSynchronize(sc));
         HIP_TRY(hipStreamSynchronize(c->s_out));
-        HIP_TRY(c->stage.ensure((size_t)kHostBufs * slab));
+        HIP_TRY(c->stage.ensure((size_t)kHostBufs * slab_al));
         c->pipe_seq = 0;
     }
-    // slabs keep their (kHostBufs) rotation across calls: each call starts at pipe_seq
+    // slabs keep their (kHostBufs) rotation across calls: each call starts at
+    // pipe_seq.  Staging buffer b sits at a fixed address (b * stage_cap),
+    // whatever this call's segment width: a call with a narrower slab (another
+    // shard size, or verify's k+p rows after an encode) must not place its
+    // buffer b inside a buffer b' that an earlier asynchronous call still
+    // reads; it waits only on ev_free[b].
+    const uint64_t stage_cap = (uint64_t)c->stage.n / kHostBufs;  // >= slab_al
     // scratch of the multi-pass paths, sized before any launch (no realloc mid-pipeline)
     if (op == HostOp::Reconstruct) e = scratch_ensure(c, c->work, (size_t)c->n * seg);
     else if (c->logm > kMaxRegLogM) e = scratch_ensure(c, c->work, (size_t)2 * c->m * seg);
@@ -1059,7 +1076,7 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
         HIP_TRY(hipStreamSynchronize(sc));
         std::vector<uint8_t *const *> d;
         for (int b = 0; b < kHostBufs; b++) {
-            for (int i = 0; i < total; i++) sets[b][i] = c->stage.p + b * slab + (uint64_t)i * seg;
+            for (int i = 0; i < total; i++) sets[b][i] = c->stage.p + b * stage_cap + (uint64_t)i * seg;
             d.push_back(sets[b].data());
         }
         e = upload_reconstruct(c, pl, d, sc);
@@ -1077,7 +1094,7 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     for (uint64_t j = 0; j < nseg; j++) {
         const int b = (int)((seq0 + j) % kHostBufs);
         const uint64_t off = j * seg, w = std::min(seg, S - off);
-        uint8_t *st = c->stage.p + b * slab;
+        uint8_t *st = c->stage.p + b * stage_cap;
         if (seq0 + j >= (uint64_t)kHostBufs) HIP_TRY(hipStreamWaitEvent(c->s_in, c->ev_free[b], 0));
         e = copy_rows(st, seg, shards, in_rows, off, w, true, c->s_in, op == HostOp::Reconstruct);
         if (e) return e;
@@ -1459,7 +1476,7 @@ int rs_reconstruct_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size
             ra.src_idx = dpl->src_idx;
             ra.dst_idx = dpl->dst_idx;
             HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
-            HIP_TRY(hipEventRecord(dpl->used, s));
+            HIP_TRY(dpl->mark_used(s));
         }
         if (!stream) HIP_TRY(hipStreamSynchronize(s));  // no caller stream: complete on return
         return RS_OK;
@@ -1666,19 +1683,19 @@ int rs_join(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshards
     size_t size = 0;
     int use = 0;
     for (int i = 0; i < c->k; i++) {  // :239-250
-        if (!shards[i] || lens[i] == 0) return RS_ERR_RECONSTRUCT_REQUIRED;
+        if (!shards[i]) return RS_ERR_RECONSTRUCT_REQUIRED;  // nil; a zero-length shard counts 0 bytes
         size += lens[i];
         use = i + 1;
         if (size >= out_size) break;
     }
     if (size < out_size) return RS_ERR_SHORT_DATA;  // :251-253
     bool dev = is_device_ptr(dst);
-    for (int i = 0; i < use && !dev; i++) dev = is_device_ptr(shards[i]);
+    for (int i = 0; i < use && !dev; i++) dev = lens[i] && is_device_ptr(shards[i]);
     size_t written = 0;
     if (!dev) {
         for (int i = 0; i < use && written < out_size; i++) {  // :256-268
             const size_t n = std::min(lens[i], out_size - written);
-            std::memcpy(dst + written, shards[i], n);
+            if (n) std::memcpy(dst + written, shards[i], n);
             written += n;
         }
         return RS_OK;
@@ -1689,7 +1706,7 @@ int rs_join(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshards
     hipStream_t s = pick_stream(c, stream);
     for (int i = 0; i < use && written < out_size; i++) {
         const size_t n = std::min(lens[i], out_size - written);
-        HIP_TRY(hipMemcpyAsync(dst + written, shards[i], n, hipMemcpyDefault, s));
+        if (n) HIP_TRY(hipMemcpyAsync(dst + written, shards[i], n, hipMemcpyDefault, s));
         written += n;
     }
     if (!stream) HIP_TRY(hipStreamSynchronize(s));

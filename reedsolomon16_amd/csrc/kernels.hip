@@ -1197,16 +1197,10 @@ constexpr uint64_t kLdsMinGrid = 512;
 #ifndef RS_ENC_ACC_REGS
 #define RS_ENC_ACC_REGS 1  // k_enc_lds keeps the accumulator in registers (even log m); 0: in LDS
 #endif
-#ifndef RS_ENC_PREFETCH
-#define RS_ENC_PREFETCH 0  // 1: k_enc_lds prefetches the next chunk's first-pass rows into registers (measured slower: 3 waves/SIMD)
-#endif
 #ifndef RS_ENC_LDS_MINBLK
-#define RS_ENC_LDS_MINBLK (RS_ENC_PREFETCH ? 3 : 4)  // k_enc_lds occupancy hint (workgroups per CU): 4 = <= 128 VGPRs
+#define RS_ENC_LDS_MINBLK 4  // k_enc_lds occupancy hint (workgroups per CU): 4 = <= 128 VGPRs
 #endif
 constexpr bool enc_acc_regs(int logm) { return RS_ENC_ACC_REGS && logm % 2 == 0 && logm >= 4; }
-#ifndef RS_REC_LDS_OUTROW
-#define RS_REC_LDS_OUTROW 0  // 1: reveal through an LDS row -> output table (1 KB more LDS per workgroup)
-#endif
 #ifndef RS_REC_NO_ZSKIP
 #define RS_REC_NO_ZSKIP 0  // 1: the from-HBM IFFT pass transforms the all-zero groups past mtrunc too (A/B)
 #endif
@@ -1234,35 +1228,18 @@ bool pick_narrow(bool automatic) {
     return o < 0 ? automatic : o == 1;
 }
 
-#ifndef RS_LDS_SWZ
-#define RS_LDS_SWZ 0  // 1: swizzled unpadded LDS rows for 128-byte GF(2^16) tiles (measured slower)
-#endif
 template <class F>
 struct LTile {
     static_assert(!F::SYM16 || F::W >= 2, "a GF(2^16) LDS tile must cover whole 64-byte blocks (W >= 2)");
     static constexpr bool W16 = F::SYM16;
     static constexpr int TB = 32 * F::W;                  // bytes of each row owned by a workgroup
-    // 128-byte GF(2^16) tiles: rows of exactly 128 B, [lo of units 0..3][hi of
-    // units 0..3], with address bits 4-7 XORed by a GF(2)-linear function of
-    // row bits 0-4 (bit 7 only from row bits >= 1, so the map is a bijection).
-    // Under the ds_read_b128 / ds_write_b128 lane groups of MI355X_MICROARCH.md
-    // §LDS, every pass of k_rec_lds / k_enc_lds (4 lanes per row, rows 1 or 4
-    // apart across lanes) is then conflict-free, against 2x the ideal LDS
-    // cycles for padded 144-byte rows with the global unit order
-    // (scripts/lds_bank_model.py).
-    static constexpr bool SWZ = W16 && F::W == 4 && RS_LDS_SWZ;
-    static constexpr int ROW = SWZ ? TB : TB + RS_LDS_PAD;  // LDS row stride
+    static constexpr int ROW = TB + RS_LDS_PAD;  // LDS row stride
     static constexpr int UB = W16 ? 8 * F::W : 4 * F::W;  // global bytes per unit
     static constexpr int U = TB / UB;                     // units per tile
     typedef typename F::Vec V;
-    __device__ static uint32_t swz(int row) {
-        const uint32_t r = (uint32_t)row;
-        return (((r & 1) ? 0x4u : 0u) ^ ((r & 4) ? 0x7u : 0u) ^ ((r & 8) ? 0xEu : 0u) ^ ((r & 16) ? 0xAu : 0u)) << 4;
-    }
     // LDS byte offset of unit u's low (h = 0) or high (h = 1) half in `row`
     __device__ static uint32_t loff(int row, int u, int h) {
-        if constexpr (SWZ) return ((uint32_t)row * TB + (uint32_t)u * 16 + 64u * h) ^ swz(row);
-        else return (uint32_t)(row * ROW + F::off(u) + 32 * h);
+        return (uint32_t)(row * ROW + F::off(u) + 32 * h);
     }
     __device__ static V get(const uint8_t *lds, int row, int u) {
         V v;
@@ -1386,13 +1363,7 @@ __device__ __forceinline__ void cfor(Fn &&f) {
 // global loads a kernel has in flight (the encoder's next-chunk prefetch) are
 // not drained at every pass as __syncthreads() would.  The passes communicate
 // only through LDS; global stores are never read back inside a launch.
-__device__ __forceinline__ void lds_sync() {
-#if RS_ENC_PREFETCH
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
-    __syncthreads();  // the measured default (no loads to keep in flight)
-#endif
-}
+__device__ __forceinline__ void lds_sync() { __syncthreads(); }
 
 // One radix-4 pass (rows i, i+d, i+2d, i+3d; twiddles m01, m02, m23 at
 // tw + 3*g) over the active groups, or a radix-2 pass.  in(row, u) supplies
@@ -1530,14 +1501,6 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     constexpr int N = 1 << LOGN, U = L::U;
     constexpr int K = (N * U + 255) / 256;  // derivative outputs per thread
     __shared__ __attribute__((aligned(16))) uint8_t lds[N * L::ROW];
-#if RS_REC_LDS_OUTROW
-    __shared__ int outrow[N];  // work row -> output index (reveal), -1: not revealed
-    for (int r = threadIdx.x; r < N; r += 256) outrow[r] = -1;
-    __syncthreads();
-    for (int j = threadIdx.x; j < a.nd; j += 256) outrow[a.pos[j]] = j;  // read after the IFFT's barriers
-#else
-    const int *outrow = nullptr;  // output index from the revealed-row mask (RevealIndex)
-#endif
     const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
     uint8_t *const sbase = a.base ? a.base + (uint64_t)blockIdx.y * a.stripe_stride : nullptr;  // this stripe
     // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0
@@ -1561,16 +1524,11 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     // reveal: shard = work[pos] * (modulus - errLocs[pos])
     struct Reveal {
         const RecArgs &a;
-        const int *outrow;
         uint64_t tile;
         uint8_t *sbase;
         Need nw;
         __device__ void operator()(int r, int u, const V &x) const {
-#if RS_REC_LDS_OUTROW
-            const int j = outrow[r];
-#else
-            const int j = reveal_index(nw, a.m, r);
-#endif
+            const int j = reveal_index(nw, a.m, r);  // output index from the revealed-row mask
             if (j < 0 || !L::valid(tile, a.S, u)) return;
             V v = F::zero();
             F::mul_add(v, x, a.tw_out + (uint64_t)j * F::TWD);
@@ -1580,7 +1538,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     };
     const LdsIO<FT> lio{lds};
     lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
-    const Reveal rv{a, outrow, tile, sbase, load_need(a.need)};
+    const Reveal rv{a, tile, sbase, load_need(a.need)};
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
     if constexpr (LOGN >= 3 && !RS_REC_UNFUSED_DERIV) {
         // fused with the FFT's first pass (radix-4 at dist D = N/4, one group,
@@ -1714,54 +1672,12 @@ __global__ void __launch_bounds__(256, RS_ENC_LDS_MINBLK) k_enc_lds(EncodeArgs a
             return sl;
         }();
         V ar[KF][4];
-#if RS_ENC_PREFETCH
-        // the IFFT's first pass (radix-4 at dist 1, groups of rows 4g..4g+3,
-        // lane-varying twiddles) runs here: its rows for chunk c + 1 are loaded
-        // into registers while chunk c's LDS passes run (LDS-only barriers
-        // leave the loads in flight)
-        constexpr int G0 = M / 4, KP = (G0 * L::U + 255) / 256;
-        V pf[KP][4];
-        auto prefetch = [&](int c) {
-            const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
-#pragma unroll
-            for (int k = 0; k < KP; k++) {
-                const int it = threadIdx.x + 256 * k;
-                if (it < G0 * L::U) {
-                    const int g = it / L::U, u = it - g * L::U;
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const int r = 4 * g + q;
-                        pf[k][q] = r < cnt && L::valid(tile, a.shard_size, u)
-                                       ? F::load(row_ptr(a.data, row0 + r) + soff + tile, u)
-                                       : F::zero();
-                    }
-                }
-            }
-        };
-        prefetch(0);
-#endif
         for (int c = 0; c < a.nchunks; c++) {
             const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
             const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
             const LdsIO<F> lio{cur};
-#if RS_ENC_PREFETCH
-#pragma unroll
-            for (int k = 0; k < KP; k++) {
-                const int it = threadIdx.x + 256 * k;
-                if (it < G0 * L::U) {
-                    const int g = it / L::U, u = it - g * L::U;
-                    ifft4<F, kLdsBranchFree>(pf[k][0], pf[k][1], pf[k][2], pf[k][3], tw + (uint64_t)g * 3 * F::TWD);
-#pragma unroll
-                    for (int q = 0; q < 4; q++) L::put(cur, 4 * g + q, u, pf[k][q]);
-                }
-            }
-            if (c + 1 < a.nchunks) prefetch(c + 1);
-            lds_sync();
-            lds_transform<F, true, LOGM, LdsIO<F>, LdsIO<F>, NoNeed, 1, NP - 1>(cur, cnt, tw, NoNeed{}, lio, lio);
-#else
             const ChunkIn in{a, row0, cnt, soff, tile};
             lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, NP - 1>(cur, cnt, tw, NoNeed{}, in, lio);
-#endif
 #pragma unroll
             for (int k = 0; k < KF; k++) {
                 const int it = threadIdx.x + 256 * k;
@@ -1809,260 +1725,6 @@ __global__ void __launch_bounds__(256, RS_ENC_LDS_MINBLK) k_enc_lds(EncodeArgs a
     if constexpr (VERIFY) {
         flag_mismatch(a.mismatch, bad != 0);
     }
-}
-
-// ---------------------------------------------------------------- 256-point transforms as two radix-16 register passes
-// GF(2^16) reconstruct with n = 256 (C4) and encode with m = 256 (C5).
-//
-// The LDS kernels above run a 256-point transform as four radix-4 passes, each
-// a round trip of the whole tile through LDS behind a barrier; the ablations
-// (scripts/gpu_ablate_rec.sh) put ~60 % of k_enc_lds's time and ~40 % of
-// k_rec_lds's outside the multiplies.  Here a thread holds 16 rows of one
-// 8-symbol unit in registers and runs four layers per pass:
-//   pass A: rows 16G + a (a = 0..15), layers 0-3 (the reference's radix-4
-//           passes at dist 1 and 4); twiddles per G (vector loads);
-//   pass B: rows j + 16a, layers 4-7 (dist 16 and 64); the twiddles depend
-//           only on a: compile-time slots of a wave-uniform table (scalar loads).
-// Slots: schedule.hpp ifft_slot / fft_slot (the reference's radix-4 order).
-// Groups the reference skips (r >= mtrunc) are computed on zero rows (IFFT)
-// or only produce rows that are never read (FFT): outputs are identical.
-// Pass A reads its rows straight from HBM (scaled in, for reconstruct) and
-// the reconstruct's formal derivative is fused into pass B (terms of row bits
-// 4-7 from registers, bits 0-3 from the LDS image), so a 256-point transform
-// pair costs two LDS round trips instead of nine.
-// Tile: 256 bytes of every row (16 units of 8 symbols); 256 threads = 16
-// groups x 16 units.  LDS row: [lo bytes of units 0..15][hi bytes], stride
-// 264 B (66 dwords: rows 16 apart land 32 banks apart, so pass A's ds_read_b64
-// lane groups are conflict-free).
-#ifndef RS_R16_SCHED
-#define RS_R16_SCHED 2
-#endif
-struct R16 {
-    typedef F16<2> F;  // full-field unit: loads, stores, scale-in / reveal tables
-    typedef F::Vec V;
-    static constexpr int TB = 256, U = 16, ROW = TB + 8, N = 256;
-    __device__ static V get(const uint8_t *lds, int row, int u) {
-        V v;
-        const uint8_t *p = lds + row * ROW + u * 8;
-        ldw_lds<2>(p, v.l);
-        ldw_lds<2>(p + 128, v.h);
-        return v;
-    }
-    __device__ static void put(uint8_t *lds, int row, int u, const V &v) {
-        typedef VecOf<2>::T T;
-        uint8_t *p = lds + row * ROW + u * 8;
-        *(__attribute__((address_space(3))) T *)(p) = T{v.l[0], v.l[1]};
-        *(__attribute__((address_space(3))) T *)(p + 128) = T{v.h[0], v.h[1]};
-    }
-    // unit u of the tile starting at column byte `tile` exists in a row of S bytes
-    __device__ static bool valid(uint64_t tile, uint64_t S, int u) { return tile + (uint64_t)(F::off(u) & ~63) < S; }
-};
-
-template <class Fn, int... Is>
-__device__ __forceinline__ void r16_for_impl(Fn &&f, std::integer_sequence<int, Is...>) {
-    (f(std::integral_constant<int, Is>{}), ...);
-}
-template <int N, class Fn>
-__device__ __forceinline__ void r16_for(Fn &&f) {
-    r16_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// Four layers of a 256-point IFFT (INV, ascending) or FFT (descending) on the
-// 16 rows x[a]: pass A (B = false) rows row0 + a, layers 0-3; pass B rows
-// j + 16a, layers 4-7.
-template <class FT, bool INV, bool B>
-__device__ __forceinline__ void r16_layers(typename FT::Vec (&x)[16], const uint32_t *__restrict__ tw, int row0) {
-    r16_for<4>([&](auto LI) {
-        constexpr int l = INV ? decltype(LI)::value : 3 - decltype(LI)::value;
-        r16_for<8>([&](auto Q) {
-            constexpr int q = decltype(Q)::value;
-            constexpr int a = ((q >> l) << (l + 1)) | (q & ((1 << l) - 1));
-            const uint32_t *t;
-            if constexpr (B) {
-                constexpr int slot = INV ? ifft_slot(8, 4 + l, 16 * a) : fft_slot(8, 4 + l, 16 * a);
-                t = tw + slot * FT::TWD;
-            } else {
-                t = tw + (INV ? ifft_slot(8, l, row0 + a) : fft_slot(8, l, row0 + a)) * FT::TWD;
-            }
-            // branch-free: a zero twiddle's table is all zeros (product 0), and a
-            // data-dependent branch per butterfly would serialize the table loads
-            if constexpr (INV) ifft2m<FT>(x[a], x[a + (1 << l)], t);
-            else fft2m<FT>(x[a], x[a + (1 << l)], t);
-#if RS_R16_SCHED == 1
-            __builtin_amdgcn_sched_barrier(0);  // one butterfly per scheduling region
-#endif
-        });
-#if RS_R16_SCHED == 2
-        __builtin_amdgcn_sched_barrier(0);  // one layer per scheduling region
-#endif
-    });
-}
-
-// Reconstruct (leopard16.go:432-568) of one stripe with n = 256, one 256-byte
-// tile per workgroup.  FT runs the transforms (F16S<2> when every transform
-// twiddle lies in GF(2^8), else F16<2>); scale-in / reveal use full-field tables.
-template <class FT>
-__global__ void __launch_bounds__(256, 2) k_rec_r16(RecArgs a) {
-    typedef R16::F F;
-    typedef F::Vec V;
-    constexpr int N = R16::N, U = R16::U;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[N * R16::ROW];
-    __shared__ int outrow[N];  // work row -> output index (reveal), -1: not revealed
-    const uint64_t tile = (uint64_t)blockIdx.x * R16::TB;
-    const int u = threadIdx.x & (U - 1), G = threadIdx.x >> 4;
-    outrow[threadIdx.x] = -1;
-    __syncthreads();
-    for (int j = threadIdx.x; j < a.nd; j += 256) outrow[a.pos[j]] = j;
-    const bool ok = R16::valid(tile, a.S, u);
-    V x[16];
-    // IFFT pass A, rows scaled in from HBM: work row r = shard * errLocs[r] (or 0)
-    if (16 * G < a.mtrunc) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int r = 16 * G + i;
-            x[i] = F::zero();
-            const uint8_t *src = a.src[r];
-            if (src && ok) F::mul_add(x[i], F::load(src + tile, u), a.tw_in + (uint64_t)r * F::TWD);
-        }
-        r16_layers<FT, true, false>(x, a.tw_ifft, 16 * G);
-    } else {
-#pragma unroll
-        for (int i = 0; i < 16; i++) x[i] = F::zero();
-    }
-#pragma unroll
-    for (int i = 0; i < 16; i++) R16::put(lds, 16 * G + i, u, x[i]);
-    __syncthreads();
-    // IFFT pass B on rows G + 16i
-#pragma unroll
-    for (int i = 0; i < 16; i++) x[i] = R16::get(lds, G + 16 * i, u);
-    r16_layers<FT, true, true>(x, a.tw_ifft, 0);
-#pragma unroll
-    for (int i = 0; i < 16; i++) R16::put(lds, G + 16 * i, u, x[i]);
-    __syncthreads();
-    // formal derivative, closed form out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b],
-    // r = G + 16i: bits 0-3 (other groups) from the image, bits 4-7 from registers
-    // (ascending i: x[i | 2^c] is still the input when x[i] is updated)
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-            if (!(G & (1 << b))) F::xor_into(x[i], R16::get(lds, (G | (1 << b)) + 16 * i, u));
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-            if (!(i & (1 << c))) F::xor_into(x[i], x[i | (1 << c)]);
-    }
-    // FFT pass B (layers 7-4)
-    r16_layers<FT, false, true>(x, a.tw_fft, 0);
-    __syncthreads();  // every thread has read the IFFT image
-#pragma unroll
-    for (int i = 0; i < 16; i++) R16::put(lds, G + 16 * i, u, x[i]);
-    __syncthreads();
-    // FFT pass A (layers 3-0), pruned like errorBitfield.fftDIT (leopard16.go:1215-1252),
-    // and reveal: shard = work[pos] * (modulus - errLocs[pos])
-    bool live = 16 * G < a.mtrunc;
-    if (live && a.prune) {
-        live = rows_needed(load_need(a.need), 16 * G, 16);
-    }
-    if (live) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) x[i] = R16::get(lds, 16 * G + i, u);
-        r16_layers<FT, false, false>(x, a.tw_fft, 16 * G);
-        if (ok) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int j = outrow[16 * G + i];
-                if (j >= 0) {
-                    V v = F::zero();
-                    F::mul_add(v, x[i], a.tw_out + (uint64_t)j * F::TWD);
-                    F::store(a.dst[j] + tile, u, v);
-                }
-            }
-        }
-    }
-}
-
-// Encode (leopard16.go:128-224) with m = 256, one 256-byte tile of one stripe
-// per workgroup: per chunk, pass A from HBM into the LDS image, pass B from the
-// image into the register accumulator; then FFT pass B from the accumulator,
-// pass A to the parity rows (or the verify compare).
-template <bool VERIFY>
-__global__ void __launch_bounds__(256, 2) k_enc_r16(EncodeArgs a) {
-    typedef R16::F F;
-    typedef F::Vec V;
-    constexpr int N = R16::N, U = R16::U;
-    constexpr int its = ifft_slot_count(8);
-    __shared__ __attribute__((aligned(16))) uint8_t lds[N * R16::ROW];
-    const uint64_t tile = (uint64_t)blockIdx.x * R16::TB;
-    const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
-    const int u = threadIdx.x & (U - 1), G = threadIdx.x >> 4;
-    const bool ok = R16::valid(tile, a.shard_size, u);
-    V acc[16], x[16];
-    for (int c = 0; c < a.nchunks; c++) {
-        const int row0 = c * N, cnt = a.k - row0 < N ? a.k - row0 : N;
-        const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
-        if (16 * G < cnt) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int r = 16 * G + i;
-                x[i] = (r < cnt && ok) ? F::load(row_ptr(a.data, row0 + r) + soff + tile, u) : F::zero();
-            }
-            r16_layers<F, true, false>(x, tw, 16 * G);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; i++) x[i] = F::zero();
-        }
-        if (c > 0) __syncthreads();  // the previous chunk's pass B has read the image
-#pragma unroll
-        for (int i = 0; i < 16; i++) R16::put(lds, 16 * G + i, u, x[i]);
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 16; i++) x[i] = R16::get(lds, G + 16 * i, u);
-        r16_layers<F, true, true>(x, tw, 0);
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            if (c == 0) acc[i] = x[i];
-            else F::xor_into(acc[i], x[i]);
-        }
-    }
-    r16_layers<F, false, true>(acc, a.tw_fft, 0);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 16; i++) R16::put(lds, G + 16 * i, u, acc[i]);
-    __syncthreads();
-    uint32_t bad = 0;
-    if (16 * G < a.p) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) x[i] = R16::get(lds, 16 * G + i, u);
-        r16_layers<F, false, false>(x, a.tw_fft, 16 * G);
-        if (ok) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int r = 16 * G + i;
-                if (r >= a.p) continue;
-                uint8_t *prow = row_ptr(a.parity, r) + soff + tile;
-                if constexpr (VERIFY) bad |= F::diff(x[i], F::load(prow, u));
-                else F::store(prow, u, x[i]);
-            }
-        }
-    }
-    if constexpr (VERIFY) flag_mismatch(a.mismatch, bad != 0);
-}
-
-// Opt-in (RS_R16=1): measured on MI355X (scripts/gpu_r16.sh) the radix-16
-// kernels are slower than the radix-4 LDS kernels -- C4 312 vs 193 us, C5
-// 266 vs 262 us per launch.  Two LDS round trips instead of nine do not pay
-// for what the register-resident passes cost: 8-symbol units (16 rows x 8
-// symbols fit the registers; the radix-4 kernels use 16-symbol units) double
-// the twiddle-table loads per symbol, pass A's per-group tables are
-// lane-varying vector loads, and only 2 workgroups fit a CU's LDS (8 waves,
-// against 16) to hide their latency; the m = 256 encode also spills.
-int r16_mode() {
-    const char *e = getenv("RS_R16");
-    return !e ? -1 : e[0] == '1' ? 1 : 0;
-}
-bool r16_pick(uint64_t groups) {
-    (void)groups;
-    return r16_mode() == 1;
 }
 
 template <class F, class FT, int LOGN>
@@ -2271,25 +1933,12 @@ hipError_t rec_lds_w(int bits, int logn, bool sub, const RecArgs &a, hipStream_t
     return sub ? rec_lds_f<F16<W>, F16S<W>>(logn, a, s) : rec_lds_f<F16<W>>(logn, a, s);
 }
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s) {
-    if (bits == 16 && logn == 8 && !a.base && a.nstripes <= 1 && r16_pick((a.S + R16::TB - 1) / R16::TB)) {
-        const dim3 grid((unsigned)((a.S + R16::TB - 1) / R16::TB));
-        if (sub) hipLaunchKernelGGL((k_rec_r16<F16S<2>>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_rec_r16<F16<2>>), grid, dim3(256), 0, s, a);
-        return hipGetLastError();
-    }
     const uint64_t ns = a.base && a.nstripes > 1 ? (uint64_t)a.nstripes : 1;
     const bool narrow = pick_narrow((a.S + 127) / 128 * ns < kLdsMinGrid);
     return narrow ? rec_lds_w<2>(bits, logn, sub, a, s) : rec_lds_w<4>(bits, logn, sub, a, s);
 }
 
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
-    const uint64_t r16_tiles = (a.shard_size + R16::TB - 1) / R16::TB;
-    if (bits == 16 && logm == 8 && r16_pick(r16_tiles * (uint64_t)a.nstripes)) {
-        const dim3 grid((unsigned)r16_tiles, (unsigned)a.nstripes);
-        if (verify) hipLaunchKernelGGL((k_enc_r16<true>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_enc_r16<false>), grid, dim3(256), 0, s, a);
-        return hipGetLastError();
-    }
     const bool narrow = pick_narrow((a.shard_size + 127) / 128 * (uint64_t)a.nstripes < kLdsMinGrid);
     if (narrow) return bits == 16 ? enc_lds_f<F16<2>>(logm, verify, a, s) : enc_lds_f<F8<2>>(logm, verify, a, s);
     return bits == 16 ? enc_lds_f<F16<4>>(logm, verify, a, s) : enc_lds_f<F8<4>>(logm, verify, a, s);

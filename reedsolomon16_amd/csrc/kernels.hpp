@@ -117,6 +117,11 @@ struct BsArgs {
 // schedule (encode_schedule: nchunks * ifft_slots(logm) IFFT logs, then
 // fft_slots(logm) FFT logs; entries == mod are truncated groups).
 bool encode_bs_available(int k, int p, const uint32_t *ifft_logs, const uint32_t *fft_logs, uint32_t mod);
+// Buffer offsets are 32-bit: every row the kernel addresses -- the padding
+// rows of the last chunk (read as zeros by the range check only while their
+// offset does not wrap) and the lanes of the last tile past the row end --
+// must lie below 4 GiB from the stripe's first data row.
+bool encode_bs_fits(int k, int p, uint64_t row_stride, uint64_t S);
 // cus: compute units of the device (the launcher sizes its persistent grid).
 // hipErrorNotSupported when the rows of one stripe span >= 4 GiB (32-bit buffer offsets).
 hipError_t launch_encode_bs(bool verify, const BsArgs &a, int cus, hipStream_t s);

@@ -198,6 +198,14 @@ def test_split_join_mirror_reference():
         c.join(io.BytesIO(), shards, 4 * 256 + 1)
     with pytest.raises(rs.ErrTooFewShards):
         c.join(io.BytesIO(), shards[:3], 10)
+    # a zero-length (non-nil) data shard counts 0 bytes (leopard16.go:239-250):
+    # the join reads on into the next shards, or is short
+    empty = np.zeros(0, np.uint8)
+    buf = io.BytesIO()
+    c.join(buf, [shards[0], empty] + shards[2:], 3 * 256)
+    assert buf.getvalue() == bytes(shards[0]) + bytes(shards[2]) + bytes(shards[3])
+    with pytest.raises(rs.ErrShortData):
+        c.join(io.BytesIO(), [shards[0], empty] + shards[2:], 3 * 256 + 1)
 
 
 @pytest.mark.parametrize("logm", [2, 3, 4, 5])

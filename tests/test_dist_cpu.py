@@ -139,3 +139,32 @@ def test_two_rank_byte_range(bits, k, p, S):
     for rank, good, ok_all, bad_all, rec_ok in res:
         assert good, f"rank {rank}: assembled parity differs from the whole-stripe oracle"
         assert ok_all and not bad_all and rec_ok
+
+
+@pytest.mark.parametrize("gpus,workload", [(2, "C3"), (4, "C5")])
+def test_bench_launcher_starts_n_ranks(gpus, workload):
+    """`bench.py --gpus N` without WORLD_SIZE starts N ranks itself (a
+    torch.distributed.run child) and each rank asserts WORLD_SIZE == N; the
+    gloo dry run reports every rank and their complementary byte ranges."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(gpus), "--dry-run",
+                          "--workload", workload], capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == gpus and len(res["ranks"]) == gpus
+    assert sorted(r["rank"] for r in res["ranks"]) == list(range(gpus))
+    assert all(r["world"] == gpus for r in res["ranks"])
+    spans = sorted(tuple(r["byte_range"]) for r in res["ranks"])
+    S = {"C3": 1 << 20, "C5": 256 << 10}[workload]
+    assert spans[0][0] == 0 and spans[-1][1] == S
+    assert all(b == c for (_, b), (c, _) in zip(spans, spans[1:]))
+    # and a mismatched WORLD_SIZE is refused
+    bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--dry-run"],
+                         capture_output=True, text=True, timeout=120, env=dict(env, WORLD_SIZE="2", RANK="0"), cwd=root)
+    assert bad.returncode != 0 and "WORLD_SIZE=2" in (bad.stderr + bad.stdout)

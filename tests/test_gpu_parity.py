@@ -733,14 +733,10 @@ def test_encode_async_stream_of_blocks():
     assert np.array_equal(np.stack(sh[k:]), orc.encode(16, k, p, np.stack(sh[:k])))
 
 
-# Radix-16 kernels for 256-point transforms (k_rec_r16: reconstruct with
-# n = 256; k_enc_r16: encode with m = 256), opt-in with RS_R16=1 (slower than
-# the radix-4 LDS kernels on MI355X); RS_R16=0 runs the radix-4
-# LDS kernels on the same inputs.
-@pytest.mark.parametrize("r16", ["1", "0"])
+# 256-point transforms: reconstruct with n = 256 and encode with m = 256
+# against the oracle, over several erasure classes and ragged tiles.
 @pytest.mark.parametrize("k,p,S", [(128, 32, 2048 + 64), (100, 100, 512), (190, 33, 256), (129, 64, 320)])
-def test_radix16_reconstruct(monkeypatch, r16, k, p, S):
-    monkeypatch.setenv("RS_R16", r16)
+def test_n256_reconstruct(k, p, S):
     rng = np.random.default_rng(k * 3 + p + S)
     data = rand_data(rng, k, S)
     par, c = gpu_encode(16, k, p, data)
@@ -759,10 +755,8 @@ def test_radix16_reconstruct(monkeypatch, r16, k, p, S):
             assert np.array_equal(sh[i], ref[i]), f"shard {i} vs oracle"
 
 
-@pytest.mark.parametrize("r16", ["1", "0"])
-def test_radix16_reconstruct_full_field(monkeypatch, r16):
-    """k_rec_r16<F16<2>> (transforms outside subfield coordinates, RS_NO_SUB=1)."""
-    monkeypatch.setenv("RS_R16", r16)
+def test_n256_reconstruct_full_field(monkeypatch):
+    """n = 256 reconstruct with transforms outside subfield coordinates (RS_NO_SUB=1)."""
     monkeypatch.setenv("RS_NO_SUB", "1")
     k, p, S = 128, 32, 1024
     rng = np.random.default_rng(77)
@@ -776,10 +770,8 @@ def test_radix16_reconstruct_full_field(monkeypatch, r16):
         assert np.array_equal(sh[i], full[i])
 
 
-@pytest.mark.parametrize("r16", ["1", "0"])
 @pytest.mark.parametrize("k,p,S", [(300, 256, 256 + 64), (257, 129, 256), (1024, 256, 512), (200, 200, 64)])
-def test_radix16_encode_verify(torch_dev, monkeypatch, r16, k, p, S):
-    monkeypatch.setenv("RS_R16", r16)
+def test_m256_encode_verify(torch_dev, k, p, S):
     torch = torch_dev
     rng = np.random.default_rng(k + p * 5 + S)
     B = 3
