@@ -48,6 +48,7 @@
 // are in-place inline asm so the compiler cannot rename their intermediates
 // into fresh registers, and every butterfly is a scheduling region.
 #include <algorithm>
+#include <cstdlib>
 #include <utility>
 
 #include "bs_tables.h"
@@ -492,7 +493,16 @@ hipError_t launch_hp_t(bool verify, BsArgs a, int cus, hipStream_t s) {
     a.ntiles = a.tiles_per_stripe * a.nstripes;
     a.span = (uint32_t)((uint64_t)(a.k - 1) * a.row_stride + a.S);
     a.pspan = (uint32_t)((uint64_t)(a.p - 1) * a.row_stride + a.S);
-    const int grid = std::min(a.ntiles, kHpWgPerCu<LOGM> * cus);
+    // One tile per workgroup: the hardware starts a new workgroup wherever
+    // one finishes, so the loads of starting tiles overlap the stores of
+    // finishing ones without the persistent grid's lockstep (same-box A/B,
+    // 128 C3 stripes: 4.39 -> 4.25 ms, 0.611 -> 0.631 of the HBM roofline,
+    // scripts/gpu_hpgrid.sh).  RS_HP_GRID=n (A/B only): persistent, n per CU.
+    static const int gmode = [] {
+        const char *e = getenv("RS_HP_GRID");
+        return e ? atoi(e) : 0;
+    }();
+    const int grid = gmode <= 0 ? a.ntiles : std::min(a.ntiles, gmode * cus);
     if (verify) hipLaunchKernelGGL((k_encode_hp<LOGM, true>), dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_encode_hp<LOGM, false>), dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();

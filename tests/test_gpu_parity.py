@@ -733,6 +733,35 @@ def test_encode_async_stream_of_blocks():
     assert np.array_equal(np.stack(sh[k:]), orc.encode(16, k, p, np.stack(sh[:k])))
 
 
+def test_encode_async_mixed_sizes_then_sync_verify():
+    """Async encodes of different shard sizes (a short last stripe) queued
+    back to back, then a synchronous verify and encode before any ticket is
+    waited on: the staging buffers sit at fixed addresses, so a narrower
+    call's buffer never lands inside a buffer an earlier call still reads."""
+    k, p = 20, 8
+    c = rs.New16(k, p)
+    c.set_host_segment(0)
+    rng = np.random.default_rng(7)
+    blocks, tickets = [], []
+    for S in (64 * 4000, 64 * 37, 64 * 4000, 64 * 5, 64 * 1500):
+        sh = c.alloc_aligned(S, pinned=True)
+        for i in range(k):
+            sh[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+        blocks.append(sh)
+        tickets.append(c.encode_async(sh))
+    # sync calls while the async ones are in flight
+    vsh = c.alloc_aligned(64 * 900, pinned=True)
+    for i in range(k):
+        vsh[i][:] = rng.integers(0, 256, 64 * 900, dtype=np.uint8)
+    c.encode(vsh)
+    assert c.verify(vsh)
+    for t in tickets:
+        t.wait()
+    for sh in blocks:
+        assert np.array_equal(np.stack(sh[k:]), orc.encode(16, k, p, np.stack(sh[:k])))
+    assert np.array_equal(np.stack(vsh[k:]), orc.encode(16, k, p, np.stack(vsh[:k])))
+
+
 # 256-point transforms: reconstruct with n = 256 and encode with m = 256
 # against the oracle, over several erasure classes and ragged tiles.
 @pytest.mark.parametrize("k,p,S", [(128, 32, 2048 + 64), (100, 100, 512), (190, 33, 256), (129, 64, 320)])
