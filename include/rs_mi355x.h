@@ -86,6 +86,27 @@ int rs_encode_query(rs_codec *codec, uint64_t ticket, int *done);
 /* Verify: leopard16.go:361-387 / leopard8.go:415-436.  *ok = 1 iff parity matches. */
 int rs_verify(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards, int *ok);
 
+/* Asynchronous Verify and Reconstruct for stream pipelining (rsStream16.verify
+ * streaming16.go:200-317 and reconstruct :320-468 call r.rs.Verify /
+ * r.rs.Reconstruct once per 4 MiB block): queued like rs_encode_async, so block
+ * j+1's copies overlap block j's kernels.  One ticket counter serves all three
+ * operations; the shard memory must stay valid until the ticket completes.
+ * rs_ticket_wait / rs_ticket_query work on any ticket (rs_encode_wait /
+ * rs_encode_query are the same functions).  Same validation and errors as the
+ * synchronous calls.  rs_reconstruct_async sets lens[i] = S for the shards it
+ * will rebuild at call time; when nothing is missing it returns RS_OK with
+ * *ticket = 0 (no work queued).  Rebuilt rows in pageable memory make the call
+ * synchronous (bounce slab), as for encode. */
+int rs_verify_async(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards, uint64_t *ticket);
+/* Waits for a verify ticket and reports *ok = 1 iff its parity matched.
+ * RS_ERR_INVALID_ARG for a ticket that is not a verify, or older than the last
+ * 64 tickets of the codec (its result slot has been reused). */
+int rs_verify_result(rs_codec *codec, uint64_t ticket, int *ok);
+int rs_reconstruct_async(rs_codec *codec, uint8_t *const *shards, size_t *lens, int nshards, int recover_all,
+                         uint64_t *ticket);
+int rs_ticket_wait(rs_codec *codec, uint64_t ticket);
+int rs_ticket_query(rs_codec *codec, uint64_t ticket, int *done);
+
 /* Reconstruct / ReconstructData / ReconstructSome: leopard16.go:343-358
  * (reconstruct :390-570), leopard8.go:392-407 (reconstruct :439-695).
  * recover_all = 1 (Reconstruct, or ReconstructSome with len(required)==total)

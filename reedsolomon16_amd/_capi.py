@@ -34,6 +34,11 @@ def lib() -> C.CDLL:
     L.rs_encode_wait.argtypes = [vp, C.c_uint64]
     L.rs_encode_query.argtypes = [vp, C.c_uint64, P(i32)]
     L.rs_verify.argtypes = [vp, P(vp), P(sz), i32, P(i32)]
+    L.rs_verify_async.argtypes = [vp, P(vp), P(sz), i32, P(C.c_uint64)]
+    L.rs_verify_result.argtypes = [vp, C.c_uint64, P(i32)]
+    L.rs_reconstruct_async.argtypes = [vp, P(vp), P(sz), i32, i32, P(C.c_uint64)]
+    L.rs_ticket_wait.argtypes = [vp, C.c_uint64]
+    L.rs_ticket_query.argtypes = [vp, C.c_uint64, P(i32)]
     L.rs_reconstruct.argtypes = [vp, P(vp), P(sz), i32, i32]
     L.rs_encode_idx.argtypes = [vp, vp, sz, i32, P(vp), P(sz), i32]
     L.rs_update.argtypes = [vp, P(vp), P(sz), i32, P(vp), P(sz), i32]

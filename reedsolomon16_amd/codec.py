@@ -280,7 +280,24 @@ class ReedSolomon:
         _check(self._L.rs_verify(self._h, ptrs, lens, len(shards), C.byref(ok)))
         return bool(ok.value)
 
-    def _reconstruct(self, shards: list, recover_all: bool) -> list:
+    def verify_async(self, shards: list) -> "VerifyTicket":
+        """Queue a Verify behind the codec's previous calls (rs_verify_async);
+        the ticket's result() waits and returns the verdict.  Keep `shards`
+        alive and unmodified until then."""
+        ptrs, lens, keep = _host_rows(shards)
+        t = C.c_uint64(0)
+        _check(self._L.rs_verify_async(self._h, ptrs, lens, len(shards), C.byref(t)))
+        return VerifyTicket(self, t.value, keep)
+
+    def reconstruct_async(self, shards: list, recover_all: bool = True) -> "EncodeTicket":
+        """Queue a Reconstruct (rs_reconstruct_async).  Missing entries of
+        `shards` are replaced at call time by the buffers the rebuilt shards
+        will land in; their bytes are final once the ticket's wait() returns."""
+        keep = []
+        t = self._reconstruct(shards, recover_all, ticket=True, keep=keep)
+        return EncodeTicket(self, t, keep)
+
+    def _reconstruct(self, shards: list, recover_all: bool, ticket: bool = False, keep=None):
         total = len(shards)
         S = next((len(s) for s in shards if s is not None and len(s)), 0)
         k = self.data_shards()
@@ -305,11 +322,16 @@ class ReedSolomon:
                 bufs[i] = b
                 ptrs[i] = b.ctypes.data
             lens[i] = len(s) if present else 0
-        _check(self._L.rs_reconstruct(self._h, ptrs, lens, total, int(recover_all)))
+        if ticket:
+            t = C.c_uint64(0)
+            _check(self._L.rs_reconstruct_async(self._h, ptrs, lens, total, int(recover_all), C.byref(t)))
+            keep.extend(bufs)
+        else:
+            _check(self._L.rs_reconstruct(self._h, ptrs, lens, total, int(recover_all)))
         for i in range(total):
             if lens[i] and (shards[i] is None or len(shards[i]) == 0):
                 shards[i] = bufs[i]
-        return shards
+        return t.value if ticket else shards
 
     def reconstruct(self, shards: list) -> list:
         """Reconstruct (leopard16.go:351-353): rebuild every missing shard."""
@@ -483,19 +505,30 @@ class ReedSolomon:
 
 
 class EncodeTicket:
-    """Completion handle of ReedSolomon.encode_async (holds the shard arrays alive)."""
+    """Completion handle of ReedSolomon.encode_async / reconstruct_async (holds
+    the shard arrays alive).  Ticket 0 means no work was queued."""
 
     def __init__(self, codec: ReedSolomon, ticket: int, keep):
         self.codec, self.ticket, self._keep = codec, ticket, keep
 
     def done(self) -> bool:
         d = C.c_int(0)
-        _check(self.codec._L.rs_encode_query(self.codec._h, self.ticket, C.byref(d)))
+        _check(self.codec._L.rs_ticket_query(self.codec._h, self.ticket, C.byref(d)))
         return bool(d.value)
 
     def wait(self) -> None:
-        _check(self.codec._L.rs_encode_wait(self.codec._h, self.ticket))
+        _check(self.codec._L.rs_ticket_wait(self.codec._h, self.ticket))
         self._keep = None
+
+
+class VerifyTicket(EncodeTicket):
+    """Completion handle of ReedSolomon.verify_async."""
+
+    def result(self) -> bool:
+        ok = C.c_int(0)
+        _check(self.codec._L.rs_verify_result(self.codec._h, self.ticket, C.byref(ok)))
+        self._keep = None
+        return bool(ok.value)
 
 
 def New(data_shards: int, parity_shards: int, device: Optional[int] = None) -> ReedSolomon:

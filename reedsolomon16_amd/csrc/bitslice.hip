@@ -51,16 +51,14 @@
 #include <cstdlib>
 #include <utility>
 
+#include "bs_common.hpp"
 #include "bs_tables.h"
 #include "kernels.hpp"
 #include "schedule.hpp"
 
 namespace rs {
 namespace {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) u32x4 lds_u4;
-typedef uint32_t Half[8];
+using namespace bs;
 
 // ---- slot indexing: schedule.hpp ifft_slot / fft_slot
 // The slots the round-2 m = 32 kernel hard-coded.
@@ -73,52 +71,6 @@ static_assert(fft_slot(5, 2, 8) == 7 && fft_slot(5, 1, 8) == 6 && fft_slot(5, 1,
 static_assert(ifft_slot(4, 2, 0) == 12 && ifft_slot(4, 2, 8) == 14 && ifft_slot(4, 3, 0) == 13, "m16 ifft");
 static_assert(fft_slot(4, 3, 0) == 1 && fft_slot(4, 2, 8) == 2 && fft_slot(4, 0, 6) == 8, "m16 fft");
 
-// ---- compile-time loops ----
-template <int V> using ic = std::integral_constant<int, V>;
-template <class Fn, int... Is>
-__device__ __forceinline__ void sfor_impl(Fn &&f, std::integer_sequence<int, Is...>) {
-    (f(ic<Is>{}), ...);
-}
-template <int N, class Fn>
-__device__ __forceinline__ void sfor(Fn &&f) {
-    sfor_impl(f, std::make_integer_sequence<int, N>{});
-}
-// Wave-uniform dispatch of a role-specialized pass: f(ic<R>) for R = role.
-template <class Fn, int... Is>
-__device__ __forceinline__ void dispatch_impl(int role, Fn &&f, std::integer_sequence<int, Is...>) {
-    ((role == Is ? (f(ic<Is>{}), 0) : 0), ...);
-}
-template <int N, class Fn>
-__device__ __forceinline__ void dispatch(int role, Fn &&f) {
-    dispatch_impl(role, f, std::make_integer_sequence<int, N>{});
-}
-
-// ---- bit-plane arithmetic ----
-// v ^= a  /  v ^= a ^ b, in place (v_bitop3_b32 truth table 0x96 = 3-input XOR).
-__device__ __forceinline__ void ixor(uint32_t &v, uint32_t a) { asm("v_xor_b32 %0, %1, %0" : "+v"(v) : "v"(a)); }
-__device__ __forceinline__ void ixor3(uint32_t &v, uint32_t a, uint32_t b) {
-    asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(v) : "v"(a), "v"(b));
-}
-// out ^= XOR of y[j] over the set bits j of mask (3-input XOR pairs).
-__device__ __forceinline__ void xor_net8(uint32_t &out, const Half &y, uint32_t mask) {
-    int pend = -1;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        if ((mask >> j) & 1) {
-            if (pend < 0) {
-                pend = j;
-            } else {
-                ixor3(out, y[pend], y[j]);
-                pend = -1;
-            }
-        }
-    }
-    if (pend >= 0) ixor(out, y[pend]);
-}
-__device__ __forceinline__ void xor8(Half &y, const Half &x) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) ixor(y[i], x[i]);
-}
 // x ^= y * twiddle (C >= 0: chunk C's IFFT slot; C < 0: FFT slot)
 template <class TW, int C, int SLOT>
 __device__ __forceinline__ void hp_mul_add(Half &x, const Half &y) {
@@ -145,28 +97,6 @@ __device__ __forceinline__ void hp_fft2(Half &x, Half &y) {
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// Delta swap of word-index bit k with bit-position bit k (s = 2^k, M = positions with bit k clear).
-__device__ __forceinline__ void bs_xchg(uint32_t &a, uint32_t &b, int s, uint32_t M) {
-    const uint32_t as = a >> s, bsh = b << s;
-    a = (a & M) | (bsh & ~M);
-    b = (b & ~M) | (as & M);
-}
-// One byte half of a 64-byte block (8 dwords: byte j of dword w = that byte
-// of symbol 4w + j) <-> 8 bit-planes (plane b bit 8j + w = bit b of symbol
-// 4w + j).  Three delta-swap stages; an involution.
-__device__ __forceinline__ void bs_transpose8(Half &w) {
-#ifdef RS_BS_ABL_NOTRANS
-    return;
-#endif
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const int s = 1 << k;
-        const uint32_t M = k == 0 ? 0x55555555u : k == 1 ? 0x33333333u : 0x0F0F0F0Fu;
-#pragma unroll
-        for (int a = 0; a < 8; a++)
-            if (!(a & s)) bs_xchg(w[a], w[a + s], s, M);
-    }
-}
 // Subfield coordinates of a whole row held as (lo planes, hi planes): lo ^= D(hi).
 template <class TW>
 __device__ __forceinline__ void hp_psi(Half &lo, const Half &hi) {
@@ -229,7 +159,6 @@ __device__ __forceinline__ void hp_get(uint32_t lbase, int row, Half &v) {
 // release/acquire fence, which waits for every outstanding global load
 // (vmcnt(0)) and so would drain the next chunk's prefetch at the first
 // barrier of every chunk; this waits for LDS traffic alone.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int LOGM, bool VERIFY>
 struct HpEncoder {

@@ -190,10 +190,14 @@ struct rs_codec {
     // staging-slab rotation continues across calls, so the segments of an
     // asynchronous encode queue behind the previous call's (rs_encode_async)
     uint64_t pipe_seq = 0;
-    // asynchronous encodes: ticket t completes at done_ev[t % kTickets]
+    // asynchronous calls (encode / verify / reconstruct): ticket t completes at
+    // done_ev[t % kTickets]; a verify ticket's mismatch word is slot t % kTickets
+    // of tk_dflag (device), copied to tk_hflag (pinned) by the ticket's own work
     static constexpr int kTickets = 64;
     hipEvent_t done_ev[kTickets] = {};
     uint64_t next_ticket = 1;
+    int *tk_hflag = nullptr, *tk_dflag = nullptr;
+    uint8_t tk_kind[kTickets] = {};  // HostOp of the slot's latest ticket, + 1
     // pinned bounce slabs for outputs in pageable host memory (kHostBufs x total x seg)
     uint8_t *bounce = nullptr;
     size_t bounce_n = 0;
@@ -226,6 +230,8 @@ struct rs_codec {
         if (bounce) (void)hipHostFree(bounce);
         for (int t = 0; t < kTickets; t++)
             if (done_ev[t]) (void)hipEventDestroy(done_ev[t]);
+        if (tk_hflag) (void)hipHostFree(tk_hflag);
+        if (tk_dflag) (void)hipFree(tk_dflag);
         for (int b = 0; b < kHostBufs; b++) {
             if (ev_in[b]) (void)hipEventDestroy(ev_in[b]);
             if (ev_k[b]) (void)hipEventDestroy(ev_k[b]);
@@ -752,6 +758,35 @@ int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
     return RS_OK;
 }
 
+// One launch of the n <= 256 reconstruct with a cached device plan over
+// strided shards (shard i of stripe y at base + y * stripe_stride + i * stride).
+int launch_rec_plan(rs_codec *c, DevPlan *dpl, uint8_t *base, uint64_t stride, uint64_t stripe_stride, int nstripes,
+                    uint64_t S, hipStream_t s) {
+    const int nd = (int)dpl->pl.dst_shard.size();
+    if (!nd) return RS_OK;
+    RecArgs ra{};
+    ra.pos = dpl->pos;
+    ra.tw_in = dpl->tw_in;
+    ra.tw_out = dpl->tw_out;
+    ra.tw_ifft = c->dtw_ifft.p;
+    ra.tw_fft = c->dtw_fft.p;
+    ra.S = S;
+    ra.mtrunc = c->m + c->k;
+    ra.m = c->m;
+    ra.nd = nd;
+    ra.prune = prune_enabled() ? 1 : 0;
+    std::memcpy(ra.need, dpl->need, sizeof(ra.need));
+    ra.base = base;
+    ra.stride = stride;
+    ra.stripe_stride = stripe_stride;
+    ra.nstripes = nstripes;
+    ra.src_idx = dpl->src_idx;
+    ra.dst_idx = dpl->dst_idx;
+    HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
+    HIP_TRY(dpl->mark_used(s));
+    return RS_OK;
+}
+
 // rs_reconstruct_dev with n <= 256 (one LDS-resident launch): the plan's tables
 // stay in HBM; equally strided shards (an AllocAligned slab, a torch 2-D
 // tensor) go to the kernel as base + stride, other layouts' row pointers
@@ -1010,9 +1045,20 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     const int k = c->k, total = c->total;
     std::vector<int> in_rows, out_rows;
     RecPlan pl;
+    // reconstruct with n <= 256: the pattern's tables stay in HBM (dev_plan)
+    // and every staging slab is strided (shard i at slab + i * seg), so the
+    // call uploads nothing and never waits for the previous one
+    DevPlan *dpl = nullptr;
     if (op == HostOp::Reconstruct) {
-        e = plan_reconstruct(c, present, recover_all, pl);
-        if (e) return e;
+        if (int be = build_decode_plan(c)) return be;
+        if (c->dec_ok && c->logn <= kMaxLdsLogN) {
+            e = dev_plan(c, present, recover_all, &dpl);
+            if (e) return e;
+            pl = dpl->pl;
+        } else {
+            e = plan_reconstruct(c, present, recover_all, pl);
+            if (e) return e;
+        }
         for (int i = 0; i < total; i++)
             if (present[i]) in_rows.push_back(i);
         out_rows = pl.dst_shard;
@@ -1069,7 +1115,7 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
         return RS_OK;
     };
     std::vector<std::vector<uint8_t *>> sets(kHostBufs, std::vector<uint8_t *>(total));
-    if (op == HostOp::Reconstruct) {
+    if (op == HostOp::Reconstruct && !dpl) {
         // the blob's per-set row tables point into the slabs; a reconstruct
         // waits for every queued segment before it rewrites the blob
         HIP_TRY(hipStreamSynchronize(c->s_out));
@@ -1082,11 +1128,30 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
         e = upload_reconstruct(c, pl, d, sc);
         if (e) return e;
     }
-    if (op == HostOp::Verify) HIP_TRY(hipMemsetAsync(c->dflag, 0, sizeof(int), sc));
-    // copies in must not start before this call's setup on the compute stream
-    // (reconstruct tables, verify flag); an encode has none, and waiting here
-    // would queue its copy-in behind every kernel of the previous call
-    if (op != HostOp::Encode) {
+    // a ticket is numbered up front: a verify ticket owns a mismatch word
+    const uint64_t tk = ticket ? c->next_ticket++ : 0;
+    const int tslot = (int)(tk % rs_codec::kTickets);
+    int *vflag_d = c->dflag, *vflag_h = c->hflag;
+    if (ticket) {
+        hipEvent_t &ev = c->done_ev[tslot];
+        if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        else if (tk > rs_codec::kTickets) HIP_TRY(hipEventSynchronize(ev));  // the slot's previous ticket is done
+        c->tk_kind[tslot] = (uint8_t)((int)op + 1);
+        if (op == HostOp::Verify) {
+            if (!c->tk_hflag) {
+                HIP_TRY(hipHostMalloc((void **)&c->tk_hflag, rs_codec::kTickets * sizeof(int), hipHostMallocDefault));
+                HIP_TRY(hipMalloc((void **)&c->tk_dflag, rs_codec::kTickets * sizeof(int)));
+            }
+            vflag_d = c->tk_dflag + tslot;
+            vflag_h = c->tk_hflag + tslot;
+        }
+    }
+    if (op == HostOp::Verify) HIP_TRY(hipMemsetAsync(vflag_d, 0, sizeof(int), sc));
+    // copies in must not start before this call's uploads on the compute
+    // stream (the multi-pass reconstruct's row tables point into the slabs);
+    // no other call has any, and waiting here would queue its copy-in behind
+    // every kernel of the previous call
+    if (op == HostOp::Reconstruct && !dpl) {
         HIP_TRY(hipEventRecord(c->ev_k[0], sc));
         HIP_TRY(hipStreamWaitEvent(c->s_in, c->ev_k[0], 0));
     }
@@ -1100,11 +1165,13 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
         if (e) return e;
         HIP_TRY(hipEventRecord(c->ev_in[b], c->s_in));
         HIP_TRY(hipStreamWaitEvent(sc, c->ev_in[b], 0));
-        if (op == HostOp::Reconstruct) {
+        if (op == HostOp::Reconstruct && dpl) {
+            e = launch_rec_plan(c, dpl, st, seg, 0, 1, w, sc);
+        } else if (op == HostOp::Reconstruct) {
             e = launch_reconstruct(c, pl, b, w, sc);
         } else {
             RowSet data{nullptr, st, seg}, par{nullptr, st + (uint64_t)k * seg, seg};
-            e = encode_device(c, data, par, w, 0, 1, op == HostOp::Verify ? c->dflag : nullptr, sc);
+            e = encode_device(c, data, par, w, 0, 1, op == HostOp::Verify ? vflag_d : nullptr, sc);
         }
         if (e) return e;
         HIP_TRY(hipEventRecord(c->ev_k[b], sc));
@@ -1123,7 +1190,7 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
         }
     }
     c->pipe_seq = seq0 + nseg;
-    if (op == HostOp::Verify) HIP_TRY(hipMemcpyAsync(c->hflag, c->dflag, sizeof(int), hipMemcpyDeviceToHost, sc));
+    if (op == HostOp::Verify) HIP_TRY(hipMemcpyAsync(vflag_h, vflag_d, sizeof(int), hipMemcpyDeviceToHost, sc));
     e = scratch_release(c, sc);
     if (e) return e;
     if (use_bounce && nseg) {
@@ -1131,11 +1198,8 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
         if (e) return e;
     }
     if (ticket) {
-        const uint64_t t = c->next_ticket++;
-        hipEvent_t &ev = c->done_ev[t % rs_codec::kTickets];
-        if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(ev, out_rows.empty() ? sc : c->s_out));
-        *ticket = t;
+        HIP_TRY(hipEventRecord(c->done_ev[tslot], out_rows.empty() ? sc : c->s_out));
+        *ticket = tk;
         if (async) {
             drain_guard.armed = false;
             return RS_OK;
@@ -1144,8 +1208,8 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     HIP_TRY(hipStreamSynchronize(c->s_in));
     HIP_TRY(hipStreamSynchronize(sc));
     HIP_TRY(hipStreamSynchronize(c->s_out));
-    if (op == HostOp::Verify) {
-        *ok = *(volatile int *)c->hflag == 0;
+    if (op == HostOp::Verify && ok) {
+        *ok = *(volatile int *)vflag_h == 0;
     }
     return RS_OK;
 }
@@ -1455,29 +1519,7 @@ int rs_reconstruct_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size
         // one launch: grid.y = stripe, the pattern's tables shared (dev_plan cache)
         DevPlan *dpl = nullptr;
         if (int e = dev_plan(c, pr, recover_all != 0, &dpl)) return e;
-        const int nd = (int)dpl->pl.dst_shard.size();
-        if (nd) {
-            RecArgs ra{};
-            ra.pos = dpl->pos;
-            ra.tw_in = dpl->tw_in;
-            ra.tw_out = dpl->tw_out;
-            ra.tw_ifft = c->dtw_ifft.p;
-            ra.tw_fft = c->dtw_fft.p;
-            ra.S = S;
-            ra.mtrunc = c->m + c->k;
-            ra.m = c->m;
-            ra.nd = nd;
-            ra.prune = prune_enabled() ? 1 : 0;
-            std::memcpy(ra.need, dpl->need, sizeof(ra.need));
-            ra.base = base;
-            ra.stride = row_stride;
-            ra.stripe_stride = stripe_stride;
-            ra.nstripes = (int)nstripes;
-            ra.src_idx = dpl->src_idx;
-            ra.dst_idx = dpl->dst_idx;
-            HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
-            HIP_TRY(dpl->mark_used(s));
-        }
+        if (int e = launch_rec_plan(c, dpl, base, row_stride, stripe_stride, (int)nstripes, S, s)) return e;
         if (!stream) HIP_TRY(hipStreamSynchronize(s));  // no caller stream: complete on return
         return RS_OK;
     }
@@ -1586,6 +1628,43 @@ int rs_encode_wait(rs_codec *c, uint64_t ticket) {
     return RS_OK;
 }
 
+int rs_ticket_query(rs_codec *c, uint64_t ticket, int *done) { return rs_encode_query(c, ticket, done); }
+int rs_ticket_wait(rs_codec *c, uint64_t ticket) { return rs_encode_wait(c, ticket); }
+
+int rs_verify_async(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshards, uint64_t *ticket) {
+    if (!c || !shards || !lens || !ticket) return RS_ERR_INVALID_ARG;
+    if (nshards != c->total) return RS_ERR_TOO_FEW_SHARDS;
+    int e = check_shards(lens, nshards, false);
+    if (e) return e;
+    const uint64_t S = lens[0];
+    if (S % 64) return RS_ERR_INVALID_SHARD_SIZE;
+    if (!c->enc_ok) return RS_ERR_PANIC;
+    for (int i = 0; i < nshards; i++)
+        if (!shards[i]) return RS_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (int ie = ensure_device(c)) return ie;
+    return host_pipeline(c, shards, S, HostOp::Verify, {}, true, nullptr, ticket);
+}
+
+int rs_verify_result(rs_codec *c, uint64_t ticket, int *ok) {
+    if (!c || !ok) return RS_ERR_INVALID_ARG;
+    *ok = 0;
+    int *h;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        const int slot = (int)(ticket % rs_codec::kTickets);
+        // the slot must still hold this verify ticket (not reused by a later call)
+        if (ticket == 0 || ticket >= c->next_ticket || ticket + rs_codec::kTickets < c->next_ticket ||
+            c->tk_kind[slot] != (uint8_t)((int)HostOp::Verify + 1) || !c->tk_hflag)
+            return RS_ERR_INVALID_ARG;
+        h = c->tk_hflag + slot;
+    }
+    if (int e = rs_encode_wait(c, ticket)) return e;
+    *ok = *(volatile int *)h == 0;
+    return RS_OK;
+}
+
 int rs_verify(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshards, int *ok) {
     if (!c || !shards || !lens || !ok) return RS_ERR_INVALID_ARG;
     *ok = 0;
@@ -1603,7 +1682,12 @@ int rs_verify(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshar
     return host_pipeline(c, shards, S, HostOp::Verify, {}, true, ok);
 }
 
-int rs_reconstruct(rs_codec *c, uint8_t *const *shards, size_t *lens, int nshards, int recover_all) {
+}  // extern "C"
+
+namespace {
+// rs_reconstruct / rs_reconstruct_async.  Nothing to rebuild: RS_OK with no
+// ticket issued (*ticket stays 0; waiting on ticket 0 is RS_ERR_INVALID_ARG).
+int reconstruct_host(rs_codec *c, uint8_t *const *shards, size_t *lens, int nshards, int recover_all, uint64_t *ticket) {
     if (!c || !shards || !lens) return RS_ERR_INVALID_ARG;
     if (nshards != c->total) return RS_ERR_TOO_FEW_SHARDS;
     int e = check_shards(lens, nshards, true);
@@ -1626,11 +1710,25 @@ int rs_reconstruct(rs_codec *c, uint8_t *const *shards, size_t *lens, int nshard
     if (int ie = ensure_device(c)) return ie;
     std::vector<uint8_t> pr(c->total);
     for (int i = 0; i < c->total; i++) pr[i] = lens[i] != 0;
-    e = host_pipeline(c, shards, S, HostOp::Reconstruct, pr, recover_all != 0, nullptr);
+    e = host_pipeline(c, shards, S, HostOp::Reconstruct, pr, recover_all != 0, nullptr, ticket);
     if (e) return e;
     for (int i = 0; i < end; i++)
         if (!pr[i]) lens[i] = S;
     return RS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rs_reconstruct(rs_codec *c, uint8_t *const *shards, size_t *lens, int nshards, int recover_all) {
+    return reconstruct_host(c, shards, lens, nshards, recover_all, nullptr);
+}
+
+int rs_reconstruct_async(rs_codec *c, uint8_t *const *shards, size_t *lens, int nshards, int recover_all,
+                         uint64_t *ticket) {
+    if (!ticket) return RS_ERR_INVALID_ARG;
+    *ticket = 0;
+    return reconstruct_host(c, shards, lens, nshards, recover_all, ticket);
 }
 
 int rs_split_shard_size(const rs_codec *c, size_t len, size_t *per_shard) {

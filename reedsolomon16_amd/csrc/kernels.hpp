@@ -97,6 +97,12 @@ struct RecArgs {
 // sub: GF(2^16) transforms in subfield coordinates (tw_ifft/tw_fft are
 // kTwDwords8 subfield tables; tw_in/tw_out fold in the coordinate change).
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s);
+// Bit-sliced reconstruct (csrc/bitslice_dec.hip): GF(2^16), n = 256, transforms
+// in subfield coordinates (tw_ifft / tw_fft: kTwDwords8 subfield tables,
+// tw_in / tw_out: full-field images that fold in the coordinate change), and
+// m + k <= 160 (its LDS image).
+bool rec_bs256_available(int bits, int logn, bool sub, int mtrunc);
+hipError_t launch_rec_bs256(const RecArgs &a, hipStream_t s);
 // Encode (or verify) for 2 <= logm <= 8, twiddles as for launch_encode_reg.
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 

@@ -233,3 +233,97 @@ def test_slot_functions_cover_every_slot():
         n_if = {4: 15, 5: 31}[logm]
         assert sorted(ifs) == list(range(n_if)) and sorted(ffs) == list(range(n_if))
         assert all(len(v) == 1 for v in list(ifs.values()) + list(ffs.values()))
+
+
+# ---------------------------------------------------------------- bit-sliced n = 256 decode (bitslice_dec.hip)
+def load_dectab():
+    if not os.path.exists(HDR):
+        pytest.skip("build/bs_tables.h not generated (run __graft_entry__.build())")
+    body = re.search(r"struct DecTab256 \{(.*?)\n\};", open(HDR).read(), re.S).group(1)
+
+    def arr(name):
+        blk = re.search(r"\b" + name + r"\[[^=]*= *(\{.*?\});", body, re.S).group(1)
+        return np.array([int(x) for x in re.findall(r"\d+", blk)], np.int64)
+
+    return arr("m8").reshape(8, 128, 8), arr("logs").reshape(8, 128)
+
+
+def test_dectab_matches_decoder_twiddles():
+    """DecTab256: layer L, group g holds fftSkew[g 2^(L+1) + 2^L - 1]
+    (ifftDITDecoder / fftDIT indexing, leopard16.go:573-657) and its 8x8
+    matrix in subfield coordinates (the product of each basis element < 256)."""
+    from oracle import leopard_np as lnp
+
+    F = lnp.field(16)
+    m8, logs = load_dectab()
+    for L in range(8):
+        for g in range(128):
+            if g >= 128 >> L:
+                assert logs[L, g] == F.mod
+                continue
+            lg = int(F._skew[g * (2 << L) + (1 << L) - 1])
+            assert logs[L, g] == lg, (L, g)
+            for j in range(8):
+                col = int(F.mul_log(1 << j, lg)) if lg != F.mod else 0
+                assert col < 256, "decoder twiddles lie in the subfield"
+                for i in range(8):
+                    assert ((m8[L, g, i] >> j) & 1) == ((col >> i) & 1), (L, g, i, j)
+
+
+def _layer(F, W, L, inverse):
+    """One radix-2 layer of the decoder transform over all rows (twiddle of the pair (a, a + 2^L))."""
+    n = W.shape[0]
+    for a in range(n):
+        if (a >> L) & 1:
+            continue
+        lg = int(F._skew[(a & ~((2 << L) - 1)) + (1 << L) - 1])
+        x, y = W[a], W[a + (1 << L)]
+        if inverse:
+            y ^= x
+            if lg != F.mod:
+                x ^= F.mul_log(y, lg)
+        else:
+            if lg != F.mod:
+                x ^= F.mul_log(y, lg)
+            y ^= x
+
+
+@pytest.mark.parametrize("mtrunc", [160, 129, 150])
+def test_decode_split_equals_reference_chain(mtrunc):
+    """The kernel's algebra (bitslice_dec.hip): IFFT layers 0-4, then
+    B_F (I + H) B_I u + Lo u over layers 5-7 with the derivative split
+    H = N_4..N_7 / Lo = N_0..N_3, then FFT layers 4-0, equals the reference
+    chain ifftDITDecoder -> formal derivative -> fftDIT (leopard16.go:518-540)
+    on every row < mtrunc, for zero rows past mtrunc."""
+    from oracle import leopard_np as lnp
+
+    F = lnp.field(16)
+    n, cols = 256, 6
+    rng = np.random.default_rng(mtrunc)
+    x = np.zeros((n, cols), np.int64)
+    x[:mtrunc] = rng.integers(0, 1 << 16, (mtrunc, cols))
+    ref = x.copy()
+    lnp.ifft_decoder(F, ref, mtrunc, n)
+    ref = lnp.formal_derivative(ref, n)
+    lnp.fft(F, ref, mtrunc, n)
+
+    u = x.copy()
+    for L in range(5):
+        _layer(F, u, L, True)
+    v = u.copy()
+    for L in (5, 6, 7):
+        _layer(F, v, L, True)
+    h = v.copy()  # (I + H) v, H = N_4 .. N_7
+    for r in range(n):
+        for b in range(4, 8):
+            if not (r >> b) & 1:
+                h[r] ^= v[r | (1 << b)]
+    for L in (7, 6, 5):
+        _layer(F, h, L, False)
+    for r in range(n):  # + Lo u
+        for b in range(4):
+            if not (r >> b) & 1:
+                h[r] ^= u[r | (1 << b)]
+    for L in (4, 3, 2, 1, 0):
+        _layer(F, h, L, False)
+    assert np.array_equal(h[:mtrunc], ref[:mtrunc])

@@ -905,3 +905,62 @@ def test_reconstruct_dev_async_row_lists(torch_dev):
     st.synchronize()
     for i, rows in enumerate(calls):
         assert torch.equal(torch.stack(rows), full), f"call {i}"
+
+
+@pytest.mark.parametrize("k,p,S", [(20, 8, 64 * 40), (128, 32, 64 * 96)])
+def test_verify_and_reconstruct_async_stream_of_blocks(k, p, S):
+    """rs_verify_async / rs_reconstruct_async over a stream of 6 blocks (the
+    rsStream16.verify / reconstruct loops, streaming16.go:200-468): every
+    block's verify and reconstruct are queued before any ticket is waited on,
+    interleaved with encodes.  Missing shards are EmptyShard views of pinned
+    rows (Go's cap() reuse), so the calls return early.  One corrupted block
+    must verify False; every rebuilt block equals the oracle's."""
+    nblk = 6
+    c = rs.New16(k, p)
+    c.set_host_segment(64 * 24)
+    o = orc.Oracle(16, k, p)
+    rng = np.random.default_rng(k + p)
+    blocks = []
+    for b in range(nblk):
+        sh = c.alloc_aligned(S, pinned=True)
+        for i in range(k):
+            sh[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+        par = orc.encode(16, k, p, np.stack(sh[:k]))
+        for i in range(p):
+            sh[k + i][:] = par[i]
+        blocks.append(sh)
+    bad = 3
+    vtk = []
+    for b, sh in enumerate(blocks):
+        rows = list(sh)
+        if b == bad:
+            rows[k + 1] = rows[k + 1].copy()
+            rows[k + 1][S // 2] ^= 0x5A
+        vtk.append((c.verify_async(rows), rows))
+    rtk, work, refs = [], [], []
+    for b, sh in enumerate(blocks):
+        pinned = c.alloc_aligned(S, pinned=True)
+        er = sorted(rng.choice(k + p, int(rng.integers(1, p + 1)), replace=False).tolist())
+        rows = [rs.EmptyShard(pinned[i]) if i in er else sh[i].copy() for i in range(k + p)]
+        refs.append([None if i in er else sh[i].copy() for i in range(k + p)])
+        rtk.append(c.reconstruct_async(rows, recover_all=(b % 2 == 0)))
+        work.append((rows, er, b % 2 == 0))
+    for b, (t, _) in enumerate(vtk):
+        assert t.result() == (b != bad), f"block {b}"
+    for t in rtk[::-1]:
+        t.wait()
+    assert all(t.done() for t in rtk)
+    for b, (rows, er, all_) in enumerate(work):
+        e, ref = o.reconstruct(refs[b], all_)
+        assert e == 0
+        for i in range(k + p):
+            if i in er and not all_ and i >= k:
+                continue
+            assert np.array_equal(np.asarray(rows[i]), ref[i]), f"block {b} shard {i}"
+            assert np.array_equal(np.asarray(rows[i]), blocks[b][i]), f"block {b} shard {i}"
+    # a verify ticket older than the 64-slot result ring is refused
+    old = vtk[0][0].ticket
+    for _ in range(70):
+        c.verify_async(list(blocks[0])).wait()
+    with pytest.raises(rs.codec.RSError):
+        rs.codec.VerifyTicket(c, old, None).result()
