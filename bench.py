@@ -31,7 +31,7 @@ around the timed launches, divided by their count).  `single_stripe` repeats
 the kernel timing with one stripe per launch (the reference's Encode
 granularity).  Resident rows sit at a stride of row bytes + --row-pad (3 KiB
 by default); `unpadded_rows` times the same launch on rows
-packed exactly one row length apart.  `cpu_baseline` times the reference-equivalent AVX2 port of the
+packed exactly one row length apart.  `cpu_baseline` times the reference-equivalent AVX2 and AVX-512 ports of the
 encode (oracle/leopard_ref.c, test/bench infrastructure) on a bounded sample:
 1 thread (the reference is single-threaded per call) and N threads over byte
 ranges.
@@ -50,8 +50,11 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
 def cpu_baseline(K, P, S, seconds: float, threads: int):
-    """Reference-equivalent AVX2 port (oracle/leopard_ref.c orc16_encode_simd),
-    same geometry, one stripe per call; scalar Ref oracle if AVX2 is absent."""
+    """Reference-equivalent SIMD ports (oracle/leopard_ref.c orc16_encode_simd_isa:
+    AVX2 like ifftDIT4_avx2, AVX-512 like ifftDIT4_avx512_*), same geometry,
+    one stripe per call, each ISA the CPU runs at 1 thread and N threads;
+    `value` is the widest ISA at N threads (the reference picks the widest,
+    galois_amd64.go:192).  Scalar Ref oracle if AVX2 is absent."""
     import numpy as np
 
     from oracle import orc
@@ -59,39 +62,50 @@ def cpu_baseline(K, P, S, seconds: float, threads: int):
     rng = np.random.default_rng(0x5EED)
     data = rng.integers(0, 256, (K, S), dtype=np.uint8)
     par = np.zeros((P, S), np.uint8)
-    simd = orc.simd_available()
+    isas = orc.simd_isas()
 
-    def run(th):
-        if simd:
-            orc.encode_simd(K, P, data, th, par)
-        else:
-            orc.encode(16, K, P, data)
+    def rate(isa, th, budget):
+        def run():
+            if isa:
+                orc.encode_simd(K, P, data, th, par, isa=isa)
+            else:
+                orc.encode(16, K, P, data)
 
-    def rate(th, budget):
-        run(th)  # warm (tables, page faults)
+        run()  # warm (tables, page faults)
         n, t0 = 0, time.perf_counter()
         while True:
-            run(th)
+            run()
             n += 1
             el = time.perf_counter() - t0
             if el >= budget:
                 return n, el
 
-    n1, el1 = rate(1, seconds / 2)
-    out = {"value": None, "unit": "GiB/s", "cores": 1, "kind": "port",
-           "single_thread": round(n1 * K * S / el1 / 2**30, 4)}
-    if simd and threads > 1:
-        nN, elN = rate(threads, seconds / 2)
-        out["value"] = round(nN * K * S / elN / 2**30, 4)
-        out["cores"] = threads
-        out["sample"] = (f"{K}+{P} x {S >> 10} KiB stripe, AVX2 nibble-table port of the reference encode "
-                         f"(oracle/leopard_ref.c, -O3): {n1} encodes on 1 thread in {el1:.1f} s, "
-                         f"{nN} encodes on {threads} threads (byte ranges) in {elN:.1f} s")
-    else:
-        out["value"] = out["single_thread"]
-        out["sample"] = (f"{K}+{P} x {S >> 10} KiB stripe, {'AVX2 port' if simd else 'scalar Ref oracle'}, "
-                         f"{n1} encodes on 1 thread in {el1:.1f} s")
-    return out
+    if not isas:
+        n1, el1 = rate(None, 1, seconds)
+        v = round(n1 * K * S / el1 / 2**30, 4)
+        return {"value": v, "unit": "GiB/s", "cores": 1, "kind": "port", "isa": "scalar", "single_thread": v,
+                "sample": f"{K}+{P} x {S >> 10} KiB stripe, scalar Ref oracle, {n1} encodes on 1 thread in {el1:.1f} s"}
+    budget = seconds / (2 * len(isas))
+    by_isa, notes = {}, []
+    for isa in isas:
+        n1, el1 = rate(isa, 1, budget)
+        e = {"kind": "port", "isa": isa, "single_thread": round(n1 * K * S / el1 / 2**30, 4)}
+        note = f"{isa}: {n1} encodes on 1 thread in {el1:.1f} s"
+        if threads > 1:
+            nN, elN = rate(isa, threads, budget)
+            e["threads"] = threads
+            e["value"] = round(nN * K * S / elN / 2**30, 4)
+            note += f", {nN} on {threads} threads (byte ranges) in {elN:.1f} s"
+        else:
+            e["value"] = e["single_thread"]
+        by_isa[isa] = e
+        notes.append(note)
+    top = by_isa[isas[-1]]
+    return {"value": top["value"], "unit": "GiB/s", "cores": threads if threads > 1 else 1, "kind": "port",
+            "isa": top["isa"], "single_thread": top["single_thread"], "by_isa": by_isa,
+            "sample": (f"{K}+{P} x {S >> 10} KiB stripe, nibble-table ports of the reference encode "
+                       f"(oracle/leopard_ref.c, -O3; AVX-512 = VL + VPTERNLOGD like ifftDIT4_avx512_*): "
+                       + "; ".join(notes))}
 
 
 def load_traffic(kernel_name: str, workload: str, stripes: int):

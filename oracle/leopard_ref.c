@@ -1059,7 +1059,6 @@ uint8_t orc8_mul_log(uint8_t a, uint8_t log_b) { return mul_log8(a, log_b); }
 #include <immintrin.h>
 #include <pthread.h>
 
-#define AVX2_FN __attribute__((target("avx2")))
 static uint8_t (*mul256)[128]; /* [log_m][128]: lo tables [i*16+x], hi tables [64+i*16+x] */
 
 static int init_mul256(void) {
@@ -1077,152 +1076,47 @@ static int init_mul256(void) {
 }
 
 typedef struct { __m256i lo[4], hi[4]; } tab256_t;
-AVX2_FN static inline void tab_load(tab256_t *t, uint16_t log_m) {
-    const uint8_t *p = mul256[log_m];
-    for (int i = 0; i < 4; i++) {
-        t->lo[i] = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)(p + i * 16)));
-        t->hi[i] = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)(p + 64 + i * 16)));
-    }
-}
-/* (plo, phi) = (lo, hi) * m for 32 symbols */
-AVX2_FN static inline void mul32(const tab256_t *t, __m256i lo, __m256i hi, __m256i *plo, __m256i *phi) {
-    const __m256i mask = _mm256_set1_epi8(0x0F);
-    const __m256i n0 = _mm256_and_si256(lo, mask), n1 = _mm256_and_si256(_mm256_srli_epi64(lo, 4), mask);
-    const __m256i n2 = _mm256_and_si256(hi, mask), n3 = _mm256_and_si256(_mm256_srli_epi64(hi, 4), mask);
-    *plo = _mm256_xor_si256(_mm256_xor_si256(_mm256_shuffle_epi8(t->lo[0], n0), _mm256_shuffle_epi8(t->lo[1], n1)),
-                            _mm256_xor_si256(_mm256_shuffle_epi8(t->lo[2], n2), _mm256_shuffle_epi8(t->lo[3], n3)));
-    *phi = _mm256_xor_si256(_mm256_xor_si256(_mm256_shuffle_epi8(t->hi[0], n0), _mm256_shuffle_epi8(t->hi[1], n1)),
-                            _mm256_xor_si256(_mm256_shuffle_epi8(t->hi[2], n2), _mm256_shuffle_epi8(t->hi[3], n3)));
-}
 typedef struct { __m256i lo, hi; } blk_t;
-AVX2_FN static inline blk_t ld(const uint8_t *p) { blk_t b = {_mm256_loadu_si256((const __m256i *)p), _mm256_loadu_si256((const __m256i *)(p + 32))}; return b; }
-AVX2_FN static inline void st(uint8_t *p, blk_t b) { _mm256_storeu_si256((__m256i *)p, b.lo); _mm256_storeu_si256((__m256i *)(p + 32), b.hi); }
-AVX2_FN static inline blk_t bx(blk_t a, blk_t b) { blk_t r = {_mm256_xor_si256(a.lo, b.lo), _mm256_xor_si256(a.hi, b.hi)}; return r; }
-/* IFFT butterfly y ^= x; x ^= y*m (t == NULL: XOR only) */
-AVX2_FN static inline void ib2(const tab256_t *t, blk_t *x, blk_t *y) {
-    *y = bx(*y, *x);
-    if (t) { blk_t p; mul32(t, y->lo, y->hi, &p.lo, &p.hi); *x = bx(*x, p); }
-}
-/* FFT butterfly x ^= y*m; y ^= x */
-AVX2_FN static inline void fb2(const tab256_t *t, blk_t *x, blk_t *y) {
-    if (t) { blk_t p; mul32(t, y->lo, y->hi, &p.lo, &p.hi); *x = bx(*x, p); }
-    *y = bx(*y, *x);
-}
-
-/* ifftDIT4 fused per 64-byte block over [lo, hi) of 4 rows */
-AVX2_FN static void ifft4_simd(uint8_t **w, int dist, uint16_t m01, uint16_t m23, uint16_t m02, size_t lo, size_t hi) {
-    tab256_t t01, t23, t02;
-    if (m01 != MOD16) tab_load(&t01, m01);
-    if (m23 != MOD16) tab_load(&t23, m23);
-    if (m02 != MOD16) tab_load(&t02, m02);
-    const tab256_t *p01 = m01 != MOD16 ? &t01 : NULL, *p23 = m23 != MOD16 ? &t23 : NULL, *p02 = m02 != MOD16 ? &t02 : NULL;
-    uint8_t *r0 = w[0], *r1 = w[dist], *r2 = w[2 * dist], *r3 = w[3 * dist];
-    for (size_t o = lo; o < hi; o += 64) {
-        blk_t a = ld(r0 + o), b = ld(r1 + o), c = ld(r2 + o), d = ld(r3 + o);
-        ib2(p01, &a, &b);
-        ib2(p23, &c, &d);
-        ib2(p02, &a, &c);
-        ib2(p02, &b, &d);
-        st(r0 + o, a); st(r1 + o, b); st(r2 + o, c); st(r3 + o, d);
-    }
-}
-AVX2_FN static void fft4_simd(uint8_t **w, int dist, uint16_t m01, uint16_t m23, uint16_t m02, size_t lo, size_t hi) {
-    tab256_t t01, t23, t02;
-    if (m01 != MOD16) tab_load(&t01, m01);
-    if (m23 != MOD16) tab_load(&t23, m23);
-    if (m02 != MOD16) tab_load(&t02, m02);
-    const tab256_t *p01 = m01 != MOD16 ? &t01 : NULL, *p23 = m23 != MOD16 ? &t23 : NULL, *p02 = m02 != MOD16 ? &t02 : NULL;
-    uint8_t *r0 = w[0], *r1 = w[dist], *r2 = w[2 * dist], *r3 = w[3 * dist];
-    for (size_t o = lo; o < hi; o += 64) {
-        blk_t a = ld(r0 + o), b = ld(r1 + o), c = ld(r2 + o), d = ld(r3 + o);
-        fb2(p02, &a, &c);
-        fb2(p02, &b, &d);
-        fb2(p01, &a, &b);
-        fb2(p23, &c, &d);
-        st(r0 + o, a); st(r1 + o, b); st(r2 + o, c); st(r3 + o, d);
-    }
-}
-AVX2_FN static void b2_simd(int inverse, uint8_t *x, uint8_t *y, uint16_t m, size_t lo, size_t hi) {
-    tab256_t t;
-    if (m != MOD16) tab_load(&t, m);
-    const tab256_t *pt = m != MOD16 ? &t : NULL;
-    for (size_t o = lo; o < hi; o += 64) {
-        blk_t a = ld(x + o), b = ld(y + o);
-        if (inverse) ib2(pt, &a, &b); else fb2(pt, &a, &b);
-        st(x + o, a); st(y + o, b);
-    }
-}
-AVX2_FN static void xor_simd(const uint8_t *in, uint8_t *out, size_t lo, size_t hi) {
-    for (size_t o = lo; o < hi; o += 64) st(out + o, bx(ld(out + o), ld(in + o)));
-}
-
-/* The encode schedule over bytes [lo, hi) of every row (skew indices checked by the caller). */
 typedef struct { int k, p; uint8_t *const *shards; size_t lo, hi; uint8_t **work; } simd_job_t;
 
-AVX2_FN static void ifft_enc_simd(uint8_t *const *data, int mtrunc, uint8_t **work, uint8_t **xor_res, int m,
-                                  const uint16_t *skew, size_t lo, size_t hi) {
-    for (int i = 0; i < mtrunc; i++) memcpy(work[i] + lo, data[i] + lo, hi - lo);
-    for (int i = mtrunc; i < m; i++) memset(work[i] + lo, 0, hi - lo);
-    int dist = 1, dist4 = 4;
-    while (dist4 <= m) {
-        for (int r = 0; r < mtrunc; r += dist4) {
-            int iend = r + dist;
-            for (int i = r; i < iend; i++)
-                ifft4_simd(work + i, dist, skew[iend], skew[iend + dist * 2], skew[iend + dist], lo, hi);
-        }
-        dist = dist4;
-        dist4 <<= 2;
-    }
-    if (dist < m)
-        for (int i = 0; i < dist; i++) b2_simd(1, work[i], work[i + dist], skew[dist], lo, hi);
-    if (xor_res)
-        for (int i = 0; i < m; i++) xor_simd(work[i], xor_res[i], lo, hi);
-}
-AVX2_FN static void fft_simd(uint8_t **work, int mtrunc, int m, size_t lo, size_t hi) {
-    int dist4 = m, dist = m >> 2;
-    while (dist != 0) {
-        for (int r = 0; r < mtrunc; r += dist4) {
-            int iend = r + dist;
-            for (int i = r; i < iend; i++)
-                fft4_simd(work + i, dist, fftSkew[iend - 1], fftSkew[iend + dist * 2 - 1], fftSkew[iend + dist - 1], lo, hi);
-        }
-        dist4 = dist;
-        dist >>= 2;
-    }
-    if (dist4 == 2)
-        for (int r = 0; r < mtrunc; r += 2) b2_simd(0, work[r], work[r + 1], fftSkew[r], lo, hi);
-}
-static void *simd_encode_job(void *arg) {
-    simd_job_t *j = (simd_job_t *)arg;
-    const int k = j->k, p = j->p, m = ceil_pow2(p), mtrunc = m < k ? m : k;
-    const uint16_t *skew = fftSkew + (m - 1);
-    uint8_t *const *sh = j->shards;
-    ifft_enc_simd(sh, mtrunc, j->work, NULL, m, skew, j->lo, j->hi);
-    const int last = k % m;
-    if (m < k) {
-        for (int i = m; i + m <= k; i += m) {
-            sh += m;
-            skew += m;
-            ifft_enc_simd(sh, m, j->work + m, j->work, m, skew, j->lo, j->hi);
-        }
-        if (last) {
-            sh += m;
-            skew += m;
-            ifft_enc_simd(sh, last, j->work + m, j->work, m, skew, j->lo, j->hi);
-        }
-    }
-    fft_simd(j->work, p, m, j->lo, j->hi);
-    for (int i = 0; i < p; i++) memcpy(j->shards[k + i] + j->lo, j->work[i] + j->lo, j->hi - j->lo);
-    return NULL;
-}
+/* The kernels once per ISA (leopard_simd.inc): AVX2 like ifftDIT4_avx2 /
+ * fftDIT4_avx2 (galois_gen_amd64.s:123870-125661), and AVX-512 like
+ * ifftDIT4_avx512_* / fftDIT4_avx512_* (:121966-123869), which keep the
+ * 256-bit nibble-table form but hold the tables in the 16 extra registers
+ * AVX-512VL gives and fold each 3-input XOR into one VPTERNLOGD 0x96. */
+#define SIMD_NAME(f) f##_avx2
+#define SIMD_FN __attribute__((target("avx2")))
+#define XOR3(a, b, c) _mm256_xor_si256(_mm256_xor_si256(a, b), c)
+#include "leopard_simd.inc"
+#undef SIMD_NAME
+#undef SIMD_FN
+#undef XOR3
+#define SIMD_NAME(f) f##_avx512
+#define SIMD_FN __attribute__((target("avx2,avx512f,avx512vl,avx512bw")))
+#define XOR3(a, b, c) _mm256_ternarylogic_epi32(a, b, c, 0x96)
+#include "leopard_simd.inc"
+#undef SIMD_NAME
+#undef SIMD_FN
+#undef XOR3
 
-/* 1 when the CPU has AVX2 (the port needs it). */
-int orc16_simd_available(void) { __builtin_cpu_init(); return __builtin_cpu_supports("avx2") ? 1 : 0; }
+/* ISAs the CPU runs: bit 0 AVX2, bit 1 AVX-512 (F + VL + BW, what the
+ * reference's avx512 path needs, galois_amd64.go:192). */
+int orc16_simd_available(void) {
+    __builtin_cpu_init();
+    int m = __builtin_cpu_supports("avx2") ? 1 : 0;
+    if (m && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("avx512bw"))
+        m |= 2;
+    return m;
+}
 
 /* Encode with the SIMD port: same contract as orc16_encode (all rows present,
- * S % 64 == 0), geometries whose encode schedule stays inside fftSkew. */
-int orc16_encode_simd(int k, int p, uint8_t *const *shards, size_t S, int threads) {
-    if (!orc16_simd_available()) return ORC_ERR_NOT_SUPPORTED;
+ * S % 64 == 0), geometries whose encode schedule stays inside fftSkew.
+ * isa: 1 AVX2, 2 AVX-512, 0 the widest the CPU runs (the reference's own
+ * choice, reedsolomon.go option defaults). */
+int orc16_encode_simd_isa(int isa, int k, int p, uint8_t *const *shards, size_t S, int threads) {
+    const int have = orc16_simd_available();
+    if (isa == 0) isa = (have & 2) ? 2 : 1;
+    if ((isa != 1 && isa != 2) || !(have & isa)) return ORC_ERR_NOT_SUPPORTED;
     if (k <= 0 || p <= 0 || k + p > ORDER16) return ORC_ERR_INV_SHARD_NUM;
     if (S == 0 || S % 64) return ORC_ERR_INVALID_SHARD_SIZE;
     if (init_mul256()) return ORC_ERR_NOMEM;
@@ -1232,23 +1126,23 @@ int orc16_encode_simd(int k, int p, uint8_t *const *shards, size_t S, int thread
     if (threads < 1) threads = 1;
     const size_t blocks = S / 64;
     if ((size_t)threads > blocks) threads = (int)blocks;
+    void *(*job)(void *) = isa == 2 ? simd_encode_job_avx512 : simd_encode_job_avx2;
     simd_job_t *jobs = (simd_job_t *)calloc((size_t)threads, sizeof(simd_job_t));
     pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
-    uint8_t **work = alloc_rows(2 * m, S);
-    uint8_t ***wrows = (uint8_t ***)calloc((size_t)threads, sizeof(uint8_t **));
-    int e = (jobs && tid && work && wrows) ? ORC_OK : ORC_ERR_NOMEM;
-    for (int t = 0; t < threads && e == ORC_OK; t++) {
-        wrows[t] = work;  /* one work slab; threads own disjoint byte ranges of it */
+    uint8_t **work = alloc_rows(2 * m, S);  /* one work slab; threads own disjoint byte ranges of it */
+    int e = (jobs && tid && work) ? ORC_OK : ORC_ERR_NOMEM;
+    for (int t = 0; t < threads && e == ORC_OK; t++)
         jobs[t] = (simd_job_t){k, p, shards, (blocks * t / threads) * 64, (blocks * (t + 1) / threads) * 64, work};
-    }
     if (e == ORC_OK) {
-        for (int t = 1; t < threads; t++) pthread_create(&tid[t], NULL, simd_encode_job, &jobs[t]);
-        simd_encode_job(&jobs[0]);
+        for (int t = 1; t < threads; t++) pthread_create(&tid[t], NULL, job, &jobs[t]);
+        job(&jobs[0]);
         for (int t = 1; t < threads; t++) pthread_join(tid[t], NULL);
     }
     free_rows(work);
-    free(wrows);
     free(jobs);
     free(tid);
     return e;
+}
+int orc16_encode_simd(int k, int p, uint8_t *const *shards, size_t S, int threads) {
+    return orc16_encode_simd_isa(0, k, p, shards, S, threads);
 }

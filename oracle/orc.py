@@ -47,6 +47,7 @@ def lib():
         L.orc8_mul_log.argtypes = [C.c_uint8, C.c_uint8]
         L.orc8_mul_log.restype = C.c_uint8
         L.orc16_encode_simd.argtypes = [C.c_int, C.c_int, P(C.c_void_p), C.c_size_t, C.c_int]
+        L.orc16_encode_simd_isa.argtypes = [C.c_int, C.c_int, C.c_int, P(C.c_void_p), C.c_size_t, C.c_int]
         L.orc16_simd_available.restype = C.c_int
         if L.orc_init() != 0:
             raise MemoryError("oracle table init failed")
@@ -154,18 +155,28 @@ def encode(bits: int, k: int, p: int, data: np.ndarray) -> np.ndarray:
     return np.stack(shards[k:])
 
 
+SIMD_ISAS = {"avx2": 1, "avx512": 2}
+
+
 def simd_available() -> bool:
     return bool(lib().orc16_simd_available())
 
 
-def encode_simd(k: int, p: int, data: np.ndarray, threads: int = 1, parity: np.ndarray = None) -> np.ndarray:
-    """GF(2^16) encode with the reference-equivalent AVX2 port (leopard_ref.c,
-    CPU baseline only): data (k,S) uint8 -> parity (p,S); `threads` byte ranges."""
+def simd_isas() -> list:
+    """ISAs of the SIMD port this CPU runs ("avx2", "avx512")."""
+    m = lib().orc16_simd_available()
+    return [n for n, b in SIMD_ISAS.items() if m & b]
+
+
+def encode_simd(k: int, p: int, data: np.ndarray, threads: int = 1, parity: np.ndarray = None, isa: str = None) -> np.ndarray:
+    """GF(2^16) encode with the reference-equivalent SIMD port (leopard_ref.c,
+    CPU baseline only): data (k,S) uint8 -> parity (p,S); `threads` byte
+    ranges; isa "avx2" / "avx512" (None: the widest the CPU runs)."""
     S = data.shape[1]
     if parity is None:
         parity = np.zeros((p, S), np.uint8)
     arr = (C.c_void_p * (k + p))(*([data[i].ctypes.data for i in range(k)] + [parity[i].ctypes.data for i in range(p)]))
-    e = lib().orc16_encode_simd(k, p, arr, S, threads)
+    e = lib().orc16_encode_simd_isa(SIMD_ISAS[isa] if isa else 0, k, p, arr, S, threads)
     if e != 0:
         raise RuntimeError(f"simd encode error {e}")
     return parity

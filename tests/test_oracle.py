@@ -182,10 +182,12 @@ def test_golden_fixtures(name):
 
 @pytest.mark.parametrize("k,p,S,threads", [(128, 32, 64 * 33, 1), (128, 32, 64 * 33, 4), (10, 4, 4096, 3),
                                            (37, 9, 640, 2), (1024, 256, 128, 2), (3, 7, 64, 1), (200, 100, 192, 8)])
-def test_simd_port_matches_scalar_oracle(k, p, S, threads):
-    """The AVX2 port bench.py times as the CPU baseline computes the oracle's parity."""
-    if not orc.simd_available():
-        pytest.skip("no AVX2 on this CPU")
+@pytest.mark.parametrize("isa", ["avx2", "avx512"])
+def test_simd_port_matches_scalar_oracle(k, p, S, threads, isa):
+    """The SIMD ports bench.py times as the CPU baseline (AVX2, and AVX-512
+    like the reference's ifftDIT4/fftDIT4_avx512_*) compute the oracle's parity."""
+    if isa not in orc.simd_isas():
+        pytest.skip(f"no {isa} on this CPU")
     rng = np.random.default_rng(k + p + S + threads)
     data = rng.integers(0, 256, (k, S), dtype=np.uint8)
-    assert np.array_equal(orc.encode_simd(k, p, data, threads), orc.encode(16, k, p, data))
+    assert np.array_equal(orc.encode_simd(k, p, data, threads, isa=isa), orc.encode(16, k, p, data))
