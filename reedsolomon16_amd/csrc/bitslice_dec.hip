@@ -46,6 +46,8 @@
 // with m + k <= 160 (C4: 160).  Rows >= mtrunc of the decoder IFFT input are
 // zero, rows >= 160 feed no output row < m + k.
 #include <algorithm>
+#include <atomic>
+#include <climits>
 
 #include "bs_common.hpp"
 #include "bs_tables.h"
@@ -147,21 +149,31 @@ constexpr uint32_t z_after(uint32_t z, int qb) {
     return r;
 }
 
+// The launch arguments, read through an opaque pointer into the kernarg
+// segment at each use: the persistent loop would otherwise keep every field
+// it touches in SGPRs for the whole loop (hundreds of SGPR spills).
+typedef __attribute__((address_space(4))) const RecArgs cargs_t;
+
 template <bool STRIDED>
 struct Dec {
-    const RecArgs &a;
+    cargs_t *ap;        // the kernel's RecArgs (first kernel argument, kernarg offset 0)
     uint32_t V[16][8];  // A layout: V[i] = row 32w + 2i + z (byte form: row 32w + t at V[t >> 1][4 (t & 1) ..])
     int lane, w;
+    int grp;            // phase 1 / phase 3 row group: rows 32 grp .. 32 grp + 31 (A layout)
     uint32_t lbase;     // LDS byte offset of this lane's 16 bytes in row 0, plane quad 0 (+ z rows)
     uint64_t col;       // first column byte of the tile
     uint8_t *sbase;     // this stripe (strided shards), or nullptr
 
-    __device__ Dec(const RecArgs &args) : a(args) {}
+    __device__ __forceinline__ cargs_t &args() const {
+        cargs_t *p = ap;
+        asm volatile("" : "+s"(p));
+        return *p;
+    }
 
     __device__ __forceinline__ uint32_t *bytes(int t) { return &V[t >> 1][4 * (t & 1)]; }
     // work row r's source shard (src_idx / src: -1 / nullptr for a zero row),
     // as a buffer descriptor over this tile with an empty range for zero rows
-    __device__ __forceinline__ __amdgpu_buffer_rsrc_t src_rsrc(int r) const {
+    __device__ __forceinline__ __amdgpu_buffer_rsrc_t src_rsrc(cargs_t &a, int r) const {
         const uint8_t *row;
         bool live;
         if constexpr (STRIDED) {
@@ -173,15 +185,15 @@ struct Dec {
             live = row != nullptr;
             row = live ? row : (const uint8_t *)a.tw_in;
         }
-        return row_rsrc(row, live ? 0u : 1u);
+        return row_rsrc(a, row, live ? 0u : 1u);
     }
-    __device__ __forceinline__ uint8_t *dst_row(int j) const {
+    __device__ __forceinline__ uint8_t *dst_row(cargs_t &a, int j) const {
         if constexpr (STRIDED) return sbase + (uint64_t)((ci32_t *)a.dst_idx)[j] * a.stride;
         else return ((cptr_t *)a.dst)[j];
     }
     // one row's 1 KB through a buffer descriptor whose range ends at the row end
     // (empty = true: a descriptor with no range, every load reads zero)
-    __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void *row, uint32_t empty = 0) const {
+    __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(cargs_t &a, const void *row, uint32_t empty = 0) const {
         const uint32_t n = empty ? 0u : (uint32_t)std::min<uint64_t>(a.S - col, kTile);
         return __builtin_amdgcn_make_buffer_rsrc((void *)((const uint8_t *)row + col), 0, (int)n, 0x00020000);
     }
@@ -191,18 +203,22 @@ struct Dec {
         return (uint32_t)(lane & 15) * 64 + (uint32_t)(lane >> 5) * 32 + (uint32_t)((lane >> 4) & 1) * 16;
     }
 
-    // ---------------- phase 1: rows 32w .. 32w + 31
-    __device__ __forceinline__ void load_scale() {
+    // ---------------- phase 1: rows 32 grp .. 32 grp + 31
+    // all 32 row loads in flight at once, straight into the row registers
+    // (the wave's 32 KB; missing rows read as zero through an empty range)
+    __device__ __forceinline__ void load_rows() {
+        cargs_t &a = args();
         const uint32_t off = lane_off();
-        // all 32 row loads in flight at once, straight into the row registers
-        // (the wave's 32 KB; missing rows read as zero through an empty range)
         sfor<32>([&](auto T) __attribute__((always_inline)) {
             constexpr int t = decltype(T)::value;
-            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(src_rsrc(32 * w + t), off, 0, 0);
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(src_rsrc(a, 32 * grp + t), off, 0, 0);
 #pragma unroll
             for (int d = 0; d < 4; d++) V[t >> 1][4 * (t & 1) + d] = x[d];
         });
         __builtin_amdgcn_sched_barrier(0);
+    }
+    __device__ __forceinline__ void scale() {
+        cargs_t &a = args();
         sfor<32>([&](auto T) __attribute__((always_inline)) {
             constexpr int t = decltype(T)::value;
             uint32_t(&v)[8] = V[t >> 1];
@@ -212,7 +228,12 @@ struct Dec {
             swap32(v[o + 0], v[o + 2]);
             swap32(v[o + 1], v[o + 3]);
             uint32_t y[4] = {v[o], v[o + 1], v[o + 2], v[o + 3]}, s[4];
-            mul16(s, y, ctab(a.tw_in) + (uint64_t)(32 * w + t) * kTw16);  // errLocs[r], into subfield coordinates
+            cu32_t *tb = ctab(a.tw_in) + (uint64_t)(32 * grp + t) * kTw16;  // errLocs[r], into subfield coordinates
+            asm volatile("" : "+s"(tb));  // row by row: all 32 tables at once would not fit the SGPRs
+            mul16(s, y, tb);
+            // the product is due before the next row's swaps (volatile, ordered):
+            // otherwise the multiplies sink below every row's table loads
+            asm volatile("" : "+v"(s[0]), "+v"(s[1]), "+v"(s[2]), "+v"(s[3]));
 #pragma unroll
             for (int d = 0; d < 4; d++) v[o + d] = s[d];
             __builtin_amdgcn_sched_barrier(0);
@@ -220,7 +241,8 @@ struct Dec {
     }
     // IFFT layer 0 (rows 2i, 2i + 1) in byte form: y ^= x; x ^= y * t
     __device__ __forceinline__ void ifft0_bytes() {
-        cu32_t *tw = ctab(a.tw_ifft) + (uint64_t)slot0(32 * w) * kTw8;
+        cargs_t &a = args();
+        cu32_t *tw = ctab(a.tw_ifft) + (uint64_t)slot0(32 * grp) * kTw8;
         sfor<16>([&](auto I) __attribute__((always_inline)) {
             constexpr int i = decltype(I)::value;
             uint32_t *x = bytes(2 * i), *y = bytes(2 * i + 1);
@@ -233,7 +255,8 @@ struct Dec {
     }
     // FFT layer 0 in byte form: x ^= y * t; y ^= x (pairs with a revealed row)
     __device__ __forceinline__ void fft0_bytes(uint32_t nw) {
-        cu32_t *tw = ctab(a.tw_fft) + (uint64_t)(kFft0Slot + slot0(32 * w)) * kTw8;
+        cargs_t &a = args();
+        cu32_t *tw = ctab(a.tw_fft) + (uint64_t)(kFft0Slot + slot0(32 * grp)) * kTw8;
         sfor<16>([&](auto I) __attribute__((always_inline)) {
             constexpr int i = decltype(I)::value;
             if ((nw >> (2 * i)) & 3u) {
@@ -278,20 +301,7 @@ struct Dec {
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    // IFFT layers 1-4 of role W: register rows i, i + 2^(L-1) (row bit L);
-    // the twiddles depend on the role (row bits 5-7).
-    template <int W>
-    __device__ __forceinline__ void ifft_a() {
-        sfor<4>([&](auto LI) __attribute__((always_inline)) {
-            constexpr int L = 1 + decltype(LI)::value, s = 1 << (L - 1);
-            sfor<8>([&](auto Q) __attribute__((always_inline)) {
-                constexpr int q = decltype(Q)::value;
-                constexpr int i = ((q >> (L - 1)) << L) | (q & (s - 1));
-                bs_ifft2<L, ((32 * W + 2 * i) >> (L + 1))>(V[i], V[i + s]);
-            });
-        });
-    }
-    // IFFT layers 1-4 with the role w chosen per butterfly: V is live into
+    // IFFT layers 1-4 with the role grp chosen per butterfly: V is live into
     // the role choice here, and a branch per role around the whole pass left
     // the allocator holding two copies of the rows.  Each role writes
     // x ^ M y into fresh registers (no tied operands) and the result moves into x.
@@ -301,7 +311,7 @@ struct Dec {
         Half &x = V[I], &y = V[I + s];
         xor8(y, x);
         Half nx;
-        dispatch<5>(w, [&](auto W) __attribute__((always_inline)) {
+        dispatch<5>(grp, [&](auto W) __attribute__((always_inline)) {
             constexpr int g = (32 * decltype(W)::value + 2 * I) >> (L + 1);
             sfor<8>([&](auto K) __attribute__((always_inline)) {
                 constexpr int k = decltype(K)::value;
@@ -312,6 +322,34 @@ struct Dec {
         for (int k = 0; k < 8; k++) x[k] = nx[k];
         __builtin_amdgcn_sched_barrier(0);
     }
+    // FFT butterfly of layer L (1-4) on register rows I, I + 2^(L-1), the role
+    // grp chosen per butterfly as in ifft_bf_a: x ^= M y; y ^= x
+    template <int L, int I>
+    __device__ __forceinline__ void fft_bf_a() {
+        constexpr int s = 1 << (L - 1);
+        Half &x = V[I], &y = V[I + s];
+        Half nx;
+        dispatch<5>(grp, [&](auto W) __attribute__((always_inline)) {
+            constexpr int g = (32 * decltype(W)::value + 2 * I) >> (L + 1);
+            sfor<8>([&](auto K) __attribute__((always_inline)) {
+                constexpr int k = decltype(K)::value;
+                xor_net8f<DT::m8[L][g][k]>(nx[k], x[k], y);
+            });
+        });
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = nx[k];
+        xor8(y, x);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __device__ __forceinline__ void fft_a_rt() {
+        sfor<4>([&](auto LI) __attribute__((always_inline)) {
+            constexpr int L = 4 - decltype(LI)::value, s = 1 << (L - 1);
+            sfor<8>([&](auto Q) __attribute__((always_inline)) {
+                constexpr int q = decltype(Q)::value;
+                fft_bf_a<L, ((q >> (L - 1)) << L) | (q & (s - 1))>();
+            });
+        });
+    }
     __device__ __forceinline__ void ifft_a_rt() {
         sfor<4>([&](auto LI) __attribute__((always_inline)) {
             constexpr int L = 1 + decltype(LI)::value, s = 1 << (L - 1);
@@ -321,23 +359,6 @@ struct Dec {
             });
         });
     }
-    // FFT layers 4-1 of role W
-    template <int W>
-    __device__ __forceinline__ void fft_a() {
-        sfor<4>([&](auto LI) __attribute__((always_inline)) {
-            constexpr int L = 4 - decltype(LI)::value, s = 1 << (L - 1);
-            sfor<8>([&](auto Q) __attribute__((always_inline)) {
-                constexpr int q = decltype(Q)::value;
-                constexpr int i = ((q >> (L - 1)) << L) | (q & (s - 1));
-                constexpr int g = (32 * W + 2 * i) >> (L + 1);
-                // no pruning inside a wave's rows: a branch per butterfly
-                // merges modified and unmodified rows, and the allocator
-                // answers with copies of whole rows
-                bs_fft2<L, g, true>(V[i], V[i + s]);
-            });
-        });
-    }
-
     // ---------------- LDS image: row r at r * 1024, plane quad pq at + pq * 512, lane at + (lane & 31) * 16
     __device__ __forceinline__ void img_put(int row_nz, const Half &v) {  // row_nz: row without the lane's z
         uint32_t o = lbase;
@@ -371,7 +392,8 @@ struct Dec {
     // ---------------- phase 2: rows z + 2v + 16q, q = 0..15 (rows >= 160 are zero)
     static constexpr int NQ = kImgRows / 16;  // 10 rows per lane below 160
     __device__ __forceinline__ void phase2(uint32_t zmask) {
-        const int v = w;
+        int v = w;
+        asm volatile("" : "+s"(v));  // per tile: keeps the image offsets from being hoisted out of the tile loop
 #pragma unroll
         for (int q = 0; q < 16; q++) {
             if (q < NQ) img_get(2 * v + 16 * q, V[q]);
@@ -429,93 +451,200 @@ struct Dec {
         });
     }
 
-    // ---------------- phase 3 reveal: rows 32w + t revealed (nw), out = work * (mod - errLocs)
-    __device__ __forceinline__ void reveal(uint32_t nw, const Need &need) {
+    // ---------------- phase 3 reveal: rows 32 grp + t revealed (nw), out = work * (mod - errLocs)
+    __device__ __forceinline__ void reveal(uint32_t nw) {
+        cargs_t &a = args();
+        const Need need = load_need(a.need);
+        // output index of revealed row r = 32 grp + t (rec_common.hpp reveal_index):
+        // its rank among the revealed rows in the rotated order [m, n), [0, m)
+        int below = 0, below_m = 0, total = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int c = __builtin_popcount(need.w[k]);
+            total += c;
+            if (k * 32 + 32 <= a.m) below_m += c;
+            else if (k * 32 < a.m) below_m += __builtin_popcount(need.w[k] & ((1u << (a.m & 31)) - 1));
+            below += k < grp ? c : 0;
+        }
+        const int j_hi = below - below_m, j_lo = total - below_m + below;
         const uint32_t off = lane_off();
         sfor<32>([&](auto T) __attribute__((always_inline)) {
             constexpr int t = decltype(T)::value;
             if ((nw >> t) & 1u) {
-                const int r = 32 * w + t;
-                const int j = reveal_index(need, a.m, r);
+                const int r = 32 * grp + t;
+                const int j = (r >= a.m ? j_hi : j_lo) + __builtin_popcount(nw & ((1u << t) - 1u));
                 uint32_t o[4];
                 uint32_t y[4] = {bytes(t)[0], bytes(t)[1], bytes(t)[2], bytes(t)[3]};
-                mul16(o, y, ctab(a.tw_out) + (uint64_t)j * kTw16);
+                cu32_t *tb = ctab(a.tw_out) + (uint64_t)j * kTw16;
+                asm volatile("" : "+s"(tb));
+                mul16(o, y, tb);
                 swap32(o[0], o[2]);  // back to lo bytes (p = 0) / hi bytes (p = 1) of symbols 16g..16g+15
                 swap32(o[1], o[3]);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{o[0], o[1], o[2], o[3]}, row_rsrc(dst_row(j)), off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{o[0], o[1], o[2], o[3]}, row_rsrc(a, dst_row(a, j)), off, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
         });
     }
 };
 
-// A role branch starts and ends with a volatile marker of its own: the
-// branches' first and last instructions (the image loads and stores) are
-// identical across roles, and the CFG simplifier would otherwise hoist or
-// sink them into the shared block, which then has to merge every row value of
-// every role (the allocator ran out of registers).
-template <int W>
-__device__ __forceinline__ void role_mark() {
-    asm volatile("; role %0" ::"n"(W));
-}
-
-// RS_DEC_ABL: bitmask of steps left out (build experiments only; wrong results)
+// RS_DEC_ABL: bitmask of steps left out (build experiments only; wrong results):
+// 1 row loads, 2 phase-1 transform, 4 phase 2, 8 phase-3 transform, 16 reveal
 #ifndef RS_DEC_ABL
 #define RS_DEC_ABL 0
 #endif
 #define ABL(b) ((RS_DEC_ABL >> (b)) & 1)
+
+// Work plan of a workgroup's 8 waves (host-made, the same for every tile:
+// launch_rec_bs256).  Phase 1 (load, scale, IFFT layers 0-4 of a 32-row group)
+// and phase 3 (FFT layers 4-0 and reveal of a group with revealed rows) run
+// only on the groups below mtrunc, 5 at C4; each is a unit of one wave.  The
+// units go to waves so that the four SIMDs carry about the same VALU work
+// (wave w runs on SIMD w & 3), and phase 3 of tile t overlaps phase 1 of the
+// next tile, whose row loads the phase-1-only waves issue early.
+struct DecPlan {
+    uint32_t p3;   // 4 bits per wave: phase-3 group + 1 (0: none)
+    uint64_t p1;   // 5 bits per wave: mask of phase-1 groups
+    int ntx;       // column tiles per stripe
+    int ntiles;    // column tiles x stripes
+};
+
+// Persistent over tiles t = blockIdx.x + i * gridDim.x (column tile t % ntx of
+// stripe t / ntx).  Iteration i runs phases 2 and 3 of tile t_(i-1) and phase
+// 1 of tile t_i:
+//   phase 2 (all waves) -> Y into the image -> phase-3 waves read their rows ->
+//   barrier (image free) -> phase 3 of t_(i-1) || phase 1 of t_i into the image.
 template <bool STRIDED>
-__global__ void __launch_bounds__(512, 2) k_rec_bs256(RecArgs a) {
+__global__ void __launch_bounds__(512, 2) k_rec_bs256(RecArgs a, DecPlan pl) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kImgRows * kTile / 4];
-    Dec<STRIDED> d(a);
+    Dec<STRIDED> d;
+    d.ap = (cargs_t *)__builtin_amdgcn_kernarg_segment_ptr();
     d.lane = threadIdx.x & 63;
     d.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    d.col = (uint64_t)blockIdx.x * kTile;
-    d.sbase = STRIDED ? a.base + (uint64_t)blockIdx.y * a.stripe_stride : nullptr;
     const int z = d.lane >> 5;
     d.lbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)lds + (uint32_t)(d.lane & 31) * 16 +
               (uint32_t)z * 1024;
     const uint32_t zmask = z ? 0u : ~0u;
     const int w = d.w;
-    // ---- phase 1: u = IFFT layers 0-4 of the scaled rows (A layout), into the image
-    if (!ABL(9) && 32 * w < a.mtrunc) {
-        if constexpr (!ABL(0)) d.load_scale();
-        if constexpr (!ABL(1)) d.ifft0_bytes();
-        if constexpr (!ABL(2)) d.to_planes(0xFFFFu);
-        // one code path per role; the rows leave for the image inside it, so
-        // no row value has to be merged from the role branches
-        if constexpr (!ABL(3)) d.ifft_a_rt();
+    const int p3g = (int)((pl.p3 >> (4 * w)) & 15u) - 1;
+    const uint32_t p1m = (uint32_t)(pl.p1 >> (5 * w)) & 31u;
+    const int first = p1m ? __builtin_ctz(p1m) : -1;
+    uint32_t nw = 0;  // revealed rows of the phase-3 group
+    if (p3g >= 0) {
+        const Need need = load_need(a.need);
+        nw = need.w[0];
 #pragma unroll
-        for (int i = 0; i < 16; i++) d.img_put(32 * w + 2 * i, d.V[i]);
+        for (int k = 1; k < 8; k++) nw = p3g == k ? need.w[k] : nw;  // wave-uniform word select
     }
-    lds_barrier();
-    // ---- phase 2: Y = B_F (I + H) B_I u + Lo u (B layout)
-    if constexpr (!ABL(4)) d.phase2(zmask);
-    lds_barrier();  // every wave has read u
+    auto set_tile = [&](int t) {
+        const int y = t / pl.ntx;
+        d.col = (uint64_t)(t - y * pl.ntx) * kTile;
+        if constexpr (STRIDED) {
+            cargs_t &ar = d.args();
+            d.sbase = ar.base + (uint64_t)y * ar.stripe_stride;
+        } else {
+            d.sbase = nullptr;
+        }
+    };
+    int t = -1, tn = blockIdx.x;  // tile in phases 2-3, tile in phase 1
+    if (tn >= pl.ntiles) return;
+    for (;;) {
+        const bool cur = t >= 0, more = tn < pl.ntiles;
+        if (cur) {
+            // ---- phase 2: Y = B_F (I + H) B_I u + Lo u (B layout)
+            if constexpr (!ABL(2)) d.phase2(zmask);
+            lds_barrier();  // every wave has read u
+            int wt = w;
+            asm volatile("" : "+s"(wt));
 #pragma unroll
-    for (int q = 0; q < Dec<STRIDED>::NQ; q++) d.img_put(2 * w + 16 * q, d.V[q]);
-    lds_barrier();
-    // ---- phase 3: FFT layers 4-0 and reveal of the revealed rows 32w .. 32w + 31
-    const Need need = load_need(a.need);
-    uint32_t nw = need.w[0];
+            for (int q = 0; q < Dec<STRIDED>::NQ; q++) d.img_put(2 * wt + 16 * q, d.V[q]);
+            lds_barrier();
+        }
+        const bool early = more && first >= 0 && (p3g < 0 || !cur);
+        if (early) {  // a phase-1-only wave: its first group's rows are on the way during the exchange
+            set_tile(tn);
+            d.grp = first;
+            if constexpr (!ABL(0)) d.load_rows();
+        }
+        if (cur) {
+            if (p3g >= 0) {
+                int g = p3g;
+                asm volatile("" : "+s"(g));
+                d.grp = g;
 #pragma unroll
-    for (int k = 1; k < 8; k++) nw = w == k ? need.w[k] : nw;  // wave-uniform word select
-    if (!ABL(10) && 32 * w < a.mtrunc && nw) {
-        // the rows come in from the image inside each role's path (see phase 1)
-        dispatch<5>(w, [&](auto W) __attribute__((always_inline)) {
-            role_mark<decltype(W)::value>();
+                for (int i = 0; i < 16; i++) d.img_get(32 * g + 2 * i, d.V[i]);
+            }
+            lds_barrier();  // the image is free for phase 1 of the next tile
+            // ---- phase 3: FFT layers 4-0 and reveal of the revealed rows of group p3g
+            if (p3g >= 0) {
+                set_tile(t);
+                if constexpr (!ABL(3)) d.fft_a_rt();
+                // opaque per tile: the loop-invariant row tests would otherwise be
+                // hoisted out of the tile loop as 48 live 64-bit masks (SGPR spills)
+                uint32_t nwt = nw;
+                asm volatile("" : "+s"(nwt));
+                uint32_t pairs = 0;  // register rows holding a revealed row (either z)
 #pragma unroll
-            for (int i = 0; i < 16; i++) d.img_get(32 * w + 2 * i, d.V[i]);
-            if constexpr (!ABL(5)) d.template fft_a<decltype(W)::value>();
-            role_mark<decltype(W)::value>();
-        });
-        uint32_t pairs = 0;  // register rows holding a revealed row (either z)
+                for (int i = 0; i < 16; i++) pairs |= ((nwt >> (2 * i)) & 3u) ? 1u << i : 0u;
+                d.to_bytes(pairs);
+                d.fft0_bytes(nwt);
+                if constexpr (!ABL(4)) d.reveal(nwt);
+            }
+        }
+        if (more) {
+            // ---- phase 1: u = IFFT layers 0-4 of the scaled rows (A layout), into the image
+            set_tile(tn);
+            for (uint32_t m = p1m; m; m &= m - 1) {
+                const int g = __builtin_ctz(m);
+                d.grp = g;
+                if (!(early && g == first))
+                    if constexpr (!ABL(0)) d.load_rows();
+                d.scale();
+                if constexpr (!ABL(1)) d.ifft0_bytes();
+                d.to_planes(0xFFFFu);
+                if constexpr (!ABL(1)) d.ifft_a_rt();
 #pragma unroll
-        for (int i = 0; i < 16; i++) pairs |= ((nw >> (2 * i)) & 3u) ? 1u << i : 0u;
-        if constexpr (!ABL(6)) d.to_bytes(pairs);
-        if constexpr (!ABL(7)) d.fft0_bytes(nw);
-        if constexpr (!ABL(8)) d.reveal(nw, need);
+                for (int i = 0; i < 16; i++) d.img_put(32 * g + 2 * i, d.V[i]);
+            }
+        }
+        if (!more) break;
+        lds_barrier();  // u of tile tn is in the image
+        t = tn;
+        tn += gridDim.x;
     }
+}
+
+// Greedy unit placement (see DecPlan): phase-3 units (cost 1) first, one per
+// wave at most, then phase-1 units (cost 2), each on the wave whose SIMD
+// carries the least work so far (ties: the least loaded wave, then the higher
+// wave index, so that phase-1-only waves stay free to load early).
+DecPlan make_plan(const RecArgs &a) {
+    DecPlan pl{};
+    const int G = (a.mtrunc + 31) / 32;
+    int simd[4] = {0, 0, 0, 0}, load[8] = {0};
+    auto pick = [&](bool need_free_p3) {
+        int best = -1;
+        for (int w = 7; w >= 0; w--) {
+            if (need_free_p3 && ((pl.p3 >> (4 * w)) & 15u)) continue;
+            if (best < 0 || simd[w & 3] < simd[best & 3] ||
+                (simd[w & 3] == simd[best & 3] && load[w] < load[best]))
+                best = w;
+        }
+        return best;
+    };
+    for (int g = 0; g < G; g++) {
+        if (!a.need[g]) continue;
+        const int w = pick(true);
+        pl.p3 |= (uint32_t)(g + 1) << (4 * w);
+        simd[w & 3] += 1;
+        load[w] += 1;
+    }
+    for (int g = 0; g < G; g++) {
+        const int w = pick(false);
+        pl.p1 |= 1ull << (5 * w + g);
+        simd[w & 3] += 2;
+        load[w] += 2;
+    }
+    return pl;
 }
 
 }  // namespace
@@ -526,15 +655,24 @@ bool rec_bs256_available(int bits, int logn, bool sub, int mtrunc) {
 
 hipError_t launch_rec_bs256(const RecArgs &a, hipStream_t s) {
     if (a.mtrunc > kImgRows) return hipErrorNotSupported;
-    const unsigned gx = (unsigned)((a.S + kTile - 1) / kTile);
-    const int ny = a.base && a.nstripes > 1 ? a.nstripes : 1;
-    for (int y0 = 0; y0 < ny; y0 += 65535) {
-        RecArgs b = a;
-        const int cnt = std::min(65535, ny - y0);
-        if (b.base) b.base = a.base + (uint64_t)y0 * a.stripe_stride;
-        if (b.base) hipLaunchKernelGGL(k_rec_bs256<true>, dim3(gx, (unsigned)cnt), dim3(512), 0, s, b);
-        else hipLaunchKernelGGL(k_rec_bs256<false>, dim3(gx, (unsigned)cnt), dim3(512), 0, s, b);
+    static std::atomic<int> cus_of[64];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    int cus = dev < 64 ? cus_of[dev].load() : 0;
+    if (!cus) {
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        if (dev < 64) cus_of[dev].store(cus);
     }
+    DecPlan pl = make_plan(a);
+    pl.ntx = (int)((a.S + kTile - 1) / kTile);
+    const uint64_t ny = a.base && a.nstripes > 1 ? (uint64_t)a.nstripes : 1;
+    if ((uint64_t)pl.ntx * ny > (uint64_t)INT32_MAX) return hipErrorInvalidValue;
+    pl.ntiles = (int)(pl.ntx * ny);
+    const unsigned grid = (unsigned)std::min<int>(pl.ntiles, std::max(cus, 1));
+    if (a.base) hipLaunchKernelGGL(k_rec_bs256<true>, dim3(grid), dim3(512), 0, s, a, pl);
+    else hipLaunchKernelGGL(k_rec_bs256<false>, dim3(grid), dim3(512), 0, s, a, pl);
     return hipGetLastError();
 }
 

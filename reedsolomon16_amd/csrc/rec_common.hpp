@@ -43,6 +43,12 @@ __device__ __forceinline__ Need load_need(const uint32_t (&src)[8]) {
     for (int k = 0; k < 8; k++) n.w[k] = __builtin_amdgcn_readfirstlane(src[k]);
     return n;
 }
+__device__ __forceinline__ Need load_need(const __attribute__((address_space(4))) uint32_t (&src)[8]) {
+    Need n;
+#pragma unroll
+    for (int k = 0; k < 8; k++) n.w[k] = src[k];  // constant address space: scalar loads
+    return n;
+}
 
 // Output index of revealed work row r, or -1: outputs are numbered as the
 // reconstruct plan lists them (codec.cpp: erased data shards = work rows
