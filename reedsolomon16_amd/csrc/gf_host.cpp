@@ -188,6 +188,19 @@ void make_sub_twiddle(const Field &F, uint32_t log_m, uint32_t *out) {
     while (d < kTwDwords8) out[d++] = 0;
 }
 
+void make_sub_dmap(uint32_t *out) {
+    static const int off[3] = {0, 3, 6}, wid[3] = {3, 3, 2};
+    const SubCoords &sc = sub_coords();
+    int d = 0;
+    for (int g = 0; g < 3; g++) {
+        uint8_t e[8] = {0};
+        for (int x = 0; x < (1 << wid[g]); x++) e[x] = (uint8_t)sc.D((uint32_t)x << off[g]);
+        out[d++] = e[0] | (e[1] << 8) | (e[2] << 16) | ((uint32_t)e[3] << 24);
+        if (wid[g] == 3) out[d++] = e[4] | (e[5] << 8) | (e[6] << 16) | ((uint32_t)e[7] << 24);
+    }
+    while (d < kTwDwords8) out[d++] = 0;
+}
+
 std::vector<PassInfo> ifft_passes(int logm) {
     std::vector<PassInfo> v;
     const int M = 1 << logm;

@@ -73,6 +73,9 @@ inline bool in_subfield(const Field &F, uint32_t log_m) { return log_m == F.mod 
 // GF(2^8)-layout (kTwDwords8) table of "multiply by exp(log_m)" on one byte of
 // subfield coordinates; log_m == mod gives the all-zero table.  log_m at dword 5.
 void make_sub_twiddle(const Field &F, uint32_t log_m, uint32_t *out);
+// The same layout for the byte map D of the coordinate change (lo, hi) ->
+// (lo ^ D(hi), hi); applying it twice is the identity.
+void make_sub_dmap(uint32_t *out);
 // GF(2^16)-layout (kTwDwords16) table of an arbitrary GF(2)-linear map f on
 // 16-bit symbols (same group/byte layout as make_twiddle; dword 20 = 0).
 template <class Fn>

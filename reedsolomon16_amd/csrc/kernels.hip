@@ -16,6 +16,7 @@
 // Butterflies (reference semantics, galois_noasm.go:58-76, leopard16.go:660-772):
 //   IFFT: y ^= x; x ^= y*m        FFT: x ^= y*m; y ^= x
 //   log_m == modulus means a zero twiddle: XOR only (wave-uniform branch).
+#include <type_traits>
 #include <cstdlib>
 #include <utility>
 
@@ -1558,7 +1559,19 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
 // chunk's first IFFT pass reads its rows from HBM, its last XORs the results
 // into acc (chunk 0: writes acc), and the FFT's last pass writes the parity
 // rows (or compares them, verify).
-template <class F, int LOGM, bool VERIFY>
+// (lo, hi) <-> (lo ^ D(hi), hi) on every symbol of v (t: make_sub_dmap table).
+template <class F>
+__device__ __forceinline__ void sub_swap(typename F::Vec &v, const uint32_t *__restrict__ t) {
+#pragma unroll
+    for (int i = 0; i < F::W; i++) {
+        const uint32_t h = v.h[i];
+        v.l[i] = xor3(v.l[i] ^ perm(t[1], t[0], h & 0x07070707u), perm(t[3], t[2], (h >> 3) & 0x07070707u),
+                      perm(t[4], t[4], (h >> 6) & 0x03030303u));
+    }
+}
+
+// FT: the field of the final FFT (F16S: subfield coordinates, EncodeArgs::tw_fft_sub).
+template <class F, int LOGM, bool VERIFY, class FT = F>
 __global__ void __launch_bounds__(256, RS_ENC_LDS_MINBLK) k_enc_lds(EncodeArgs a) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
@@ -1586,12 +1599,15 @@ __global__ void __launch_bounds__(256, RS_ENC_LDS_MINBLK) k_enc_lds(EncodeArgs a
             L::put(acc, r, u, v);
         }
     };
+    constexpr bool SUB = !std::is_same<F, FT>::value;
     struct ParityOut {
         const EncodeArgs &a;
         uint64_t soff, tile;
         uint32_t *bad;
-        __device__ void operator()(int r, int u, const V &v) const {
+        __device__ void operator()(int r, int u, const V &v0) const {
             if (r >= a.p || !L::valid(tile, a.shard_size, u)) return;
+            V v = v0;
+            if constexpr (SUB) sub_swap<F>(v, a.tw_dmap);  // back to (lo, hi)
             uint8_t *prow = row_ptr(a.parity, r) + soff + tile;
             if constexpr (VERIFY) *bad |= F::diff(v, F::load(prow, u));
             else F::store(prow, u, v);
@@ -1635,19 +1651,23 @@ __global__ void __launch_bounds__(256, RS_ENC_LDS_MINBLK) k_enc_lds(EncodeArgs a
             lds_sync();  // the next chunk's first pass overwrites cur
         }
         uint32_t bad = 0;
+        const uint32_t *twf = SUB ? a.tw_fft_sub : a.tw_fft;
 #pragma unroll
         for (int k = 0; k < KF; k++) {
             const int it = threadIdx.x + 256 * k;
             if (it < D * L::U) {
                 const int i = it / L::U, u = it - i * L::U;
-                fft4<F>(ar[k][0], ar[k][1], ar[k][2], ar[k][3], a.tw_fft);
+                if constexpr (SUB)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) sub_swap<F>(ar[k][q], a.tw_dmap);  // into subfield coordinates
+                fft4<FT>(ar[k][0], ar[k][1], ar[k][2], ar[k][3], twf);
 #pragma unroll
                 for (int q = 0; q < 4; q++) L::put(cur, i + q * D, u, ar[k][q]);
             }
         }
         __syncthreads();
-        lds_transform<F, false, LOGM, LdsIO<F>, ParityOut, NoNeed, 1>(cur, a.p, a.tw_fft, NoNeed{}, LdsIO<F>{cur},
-                                                                       ParityOut{a, soff, tile, &bad});
+        lds_transform<FT, false, LOGM, LdsIO<FT>, ParityOut, NoNeed, 1>(cur, a.p, twf, NoNeed{}, LdsIO<FT>{cur},
+                                                                         ParityOut{a, soff, tile, &bad});
         if constexpr (VERIFY) flag_mismatch(a.mismatch, bad != 0);
         return;
     }
@@ -1693,18 +1713,33 @@ hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
-template <class F, int LOGM>
-hipError_t enc_lds_t(bool verify, const EncodeArgs &a, hipStream_t s) {
+template <class F, int LOGM, class FT>
+hipError_t enc_lds_tt(bool verify, const EncodeArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)((a.shard_size + LTile<F>::TB - 1) / LTile<F>::TB), (unsigned)a.nstripes);
     const size_t lds = (size_t)(enc_acc_regs(LOGM) ? 1 : 2) * (1 << LOGM) * LTile<F>::ROW;
     if (verify) {
-        (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((k_enc_lds<F, LOGM, true>), grid, dim3(256), lds, s, a);
+        (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, true, FT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_enc_lds<F, LOGM, true, FT>), grid, dim3(256), lds, s, a);
     } else {
-        (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((k_enc_lds<F, LOGM, false>), grid, dim3(256), lds, s, a);
+        (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, false, FT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_enc_lds<F, LOGM, false, FT>), grid, dim3(256), lds, s, a);
     }
     return hipGetLastError();
+}
+template <class F>
+struct SubOf {
+    typedef F type;
+};
+template <int W>
+struct SubOf<F16<W>> {
+    typedef F16S<W> type;
+};
+template <class F, int LOGM>
+hipError_t enc_lds_t(bool verify, const EncodeArgs &a, hipStream_t s) {
+    if constexpr (F::SYM16 && enc_acc_regs(LOGM)) {
+        if (a.tw_fft_sub && a.tw_dmap) return enc_lds_tt<F, LOGM, typename SubOf<F>::type>(verify, a, s);
+    }
+    return enc_lds_tt<F, LOGM, F>(verify, a, s);
 }
 template <class F>
 hipError_t enc_lds_f(int logm, bool verify, const EncodeArgs &a, hipStream_t s) {

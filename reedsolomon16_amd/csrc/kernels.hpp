@@ -31,6 +31,13 @@ struct EncodeArgs {
     const uint32_t *tw_ifft;  // nchunks * ifft_slots(logm) twiddle tables
     const uint32_t *tw_fft;   // fft_slots(logm) twiddle tables
     int *mismatch;            // verify: set to 1 on any parity mismatch
+    // Optional (GF(2^16), LDS kernel, even log m): the final FFT in subfield
+    // coordinates.  Every fftDIT twiddle of an m <= 256 encode is fftSkew[< 255],
+    // an element of GF(2^8) (leopard16.go:218-221), so the transform runs on
+    // (lo ^ D(hi), hi) with kTwDwords8 subfield tables (6 v_perm_b32 per product
+    // instead of 12); tw_dmap is the byte map D (make_sub_dmap).  nullptr: full field.
+    const uint32_t *tw_fft_sub;
+    const uint32_t *tw_dmap;
 };
 
 // Returns hipSuccess or the launch error.  logm in [0, 5].

@@ -42,6 +42,12 @@ HOST_CONFIGS = {
     # queued with rs_encode_async and waited at the end (async)
     "H3s_sync": (16, 128, 32, 1 << 20, "stream_sync", True),
     "H3s_async": (16, 128, 32, 1 << 20, "stream_async", True),
+    # the same stream verified (parity already written) or repaired (32 erasures
+    # per block, rebuilt into the caller's pinned rows), sync vs tickets
+    "H3vs_sync": (16, 128, 32, 1 << 20, "stream_verify_sync", True),
+    "H3vs_async": (16, 128, 32, 1 << 20, "stream_verify_async", True),
+    "H4s_sync": (16, 128, 32, 1 << 20, "stream_rec_sync", True),
+    "H4s_async": (16, 128, 32, 1 << 20, "stream_rec_async", True),
 }
 
 
@@ -64,12 +70,33 @@ def time_host(name, iters, tag):
                 sh[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
             blocks.append(sh)
 
+        if op != "stream_sync" and op != "stream_async":
+            for sh in blocks:
+                c.encode(sh)
+        erased = [set(rng.choice(k + p, p, replace=False).tolist()) for _ in range(nblk)]
+
+        def rec_view(j):
+            return [rs.EmptyShard(blocks[j][i]) if i in erased[j] else blocks[j][i] for i in range(k + p)]
+
         def run_stream():
             if op == "stream_sync":
                 for sh in blocks:
                     c.encode(sh)
-            else:
+            elif op == "stream_async":
                 ts = [c.encode_async(sh) for sh in blocks]
+                for t in ts:
+                    t.wait()
+            elif op == "stream_verify_sync":
+                for sh in blocks:
+                    assert c.verify(sh)
+            elif op == "stream_verify_async":
+                ts = [c.verify_async(sh) for sh in blocks]
+                assert all(t.result() for t in ts)
+            elif op == "stream_rec_sync":
+                for j in range(nblk):
+                    c.reconstruct(rec_view(j))
+            else:
+                ts = [c.reconstruct_async(rec_view(j)) for j in range(nblk)]
                 for t in ts:
                     t.wait()
 
