@@ -133,7 +133,11 @@ struct rs_codec {
     bool split_ok = false;            // half-wave split kernel available (GF(2^16), 4 <= m <= 32)
     bool bs_ok = false;               // bit-sliced kernel covers (k, p) (GF(2^16), m = 16 or 32)
     int cus = 0;                      // compute units of the device (persistent grids)
-    DevBuf<uint32_t> tws_ifft, tws_fft;  // its twiddle images (schedule.hpp EncodeSplit)
+    DevBuf<uint32_t> tws_ifft, tws_fft;
+    // LDS-kernel encode (GF(2^16), even log m): the final FFT's subfield tables
+    // and the coordinate-change map (EncodeArgs::tw_fft_sub / tw_dmap)
+    DevBuf<uint32_t> tw_fft_sub, tw_dmap;
+    bool fft_sub = false;  // its twiddle images (schedule.hpp EncodeSplit)
     std::string path;
 
     // decode plan (built on first reconstruct)
@@ -210,7 +214,7 @@ struct rs_codec {
             (void)hipEventSynchronize(scratch_ev);
             (void)hipEventDestroy(scratch_ev);
         }
-        tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); dtw_ifft.release(); dtw_fft.release();
+        tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); tw_fft_sub.release(); tw_dmap.release(); dtw_ifft.release(); dtw_fft.release();
         work.release(); rows.release();
         if (hflag) (void)hipHostFree(hflag);
         if (dflag) (void)hipFree(dflag);
@@ -354,6 +358,20 @@ int ensure_device(rs_codec *c) {
         if (c->bits == 16 && split_enabled()) {
             e = upload_split(c);
             if (e) return e;
+        }
+        // m <= 256: every fftDIT twiddle is fftSkew[< 255], in GF(2^8)
+        bool sub = c->bits == 16 && c->logm > kMaxRegLogM && c->logm <= kMaxLdsLogN && c->logm % 2 == 0 &&
+                   sub_enabled() && sub_coords().ok;
+        for (uint32_t l : c->enc_fft_logs) sub = sub && in_subfield(*c->F, l);
+        if (sub) {
+            std::vector<uint32_t> hf(std::max<size_t>(c->enc_fft_logs.size(), 1) * kTwDwords8, 0), dm(kTwDwords8, 0);
+            for (size_t i = 0; i < c->enc_fft_logs.size(); i++) make_sub_twiddle(*c->F, c->enc_fft_logs[i], hf.data() + i * kTwDwords8);
+            make_sub_dmap(dm.data());
+            HIP_TRY(c->tw_fft_sub.ensure(hf.size()));
+            HIP_TRY(c->tw_dmap.ensure(dm.size()));
+            HIP_TRY(hipMemcpy(c->tw_fft_sub.p, hf.data(), hf.size() * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(c->tw_dmap.p, dm.data(), dm.size() * 4, hipMemcpyHostToDevice));
+            c->fft_sub = true;
         }
     }
     c->dev_ready = true;
@@ -549,6 +567,10 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
         a.nstripes = (data.table || par.table) ? 1 : nstripes;
         a.tw_ifft = c->tw_ifft.p;
         a.tw_fft = c->tw_fft.p;
+        if (c->fft_sub) {
+            a.tw_fft_sub = c->tw_fft_sub.p;
+            a.tw_dmap = c->tw_dmap.p;
+        }
         a.mismatch = mismatch;
         HIP_TRY(launch_encode_lds(c->bits, c->logm, mismatch != nullptr, a, s));
         return RS_OK;
