@@ -33,7 +33,7 @@ def path_of(name: str):
     m = re.search(r"k_encode_split<(\d+), (false|true)>", name)
     if m:
         return f"split16-m{1 << int(m.group(1))}" + v(m.group(2))
-    m = re.search(r"k_enc_lds<rs::\(anonymous namespace\)::F(16|8)<\d+>, (\d+), (false|true)>", name)
+    m = re.search(r"k_enc_lds<rs::\(anonymous namespace\)::F(16|8)<\d+>, (\d+), (false|true)[,>]", name)
     if m:
         return f"lds-m{1 << int(m.group(2))}" + v(m.group(3))
     m = re.search(r"k_encode_reg<rs::\(anonymous namespace\)::F(16|8)<\d+>, (\d+), (false|true)", name)
