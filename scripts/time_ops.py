@@ -19,6 +19,10 @@ CONFIGS = {
     "C4e8": (16, 128, 32, 1 << 20, "reconstruct", 1, 8),
     "C5": (16, 1024, 256, 256 << 10, "encode"),
     "C5x8": (16, 1024, 256, 32 << 10, "encode"),
+    # C5 batched: 32 stripes per launch, whole rows and the 8-rank 32 KiB slice
+    "C5b32": (16, 1024, 256, 256 << 10, "encode", 32),
+    "C5x8b32": (16, 1024, 256, 32 << 10, "encode", 32),
+    "C5vb32": (16, 1024, 256, 256 << 10, "verify", 32),
     # encode batches: stripes per launch (rs_encode_dev_batch), so a small
     # stripe's kernel time is not hidden behind the per-call host cost
     "C2x16": (8, 10, 4, 1 << 20, "encode", 16),
