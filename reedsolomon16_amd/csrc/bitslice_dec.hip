@@ -16,24 +16,25 @@
 // GF(2) map on both byte halves, i.e. a fixed XOR network over 8 bit-planes.
 //
 // Tile: 1 KB of columns (16 blocks of 64 bytes) of every row of one stripe.
-// Lane l = (block b = l & 15, half h = (l >> 4) & 1, row bit 0 z = l >> 5);
-// a lane holds 16 rows x 8 planes (128 VGPRs).  One workgroup per CU (the LDS
-// image below takes all 160 KB), persistent over tiles, 12 waves (three per
-// SIMD, <= 168 VGPRs): 8 run phase 2, and the phase-1 / phase-3 units of a
-// tile go one per wave (make_plan), phase 3 of a tile overlapping phase 1 of
-// the next one.
+// Lane l = (block b = l & 15, half h = (l >> 4) & 1, row bit 0 z = l >> 5).
+// One workgroup per CU (the LDS image below takes all 160 KB), persistent
+// over tiles, 12 waves (three per SIMD, <= 168 VGPRs): 8 run phase 2; the
+// phase-1 / phase-3 units of a tile are 16-row units spread over the waves
+// (make_plan).  Waves 8-11 take no part in phase 2: they run phase 1 of the
+// next tile while waves 0-7 run phase 2 of the current one.
 //
-//   A layout: wave w = row bits 5-7, registers i = row bits 1-4.
-//   B layout: wave v = row bits 1-3, registers q = row bits 4-7.
+//   A layout: unit u = row bits 4-7, registers i = row bits 1-3 (8 rows x 8 planes).
+//   B layout: wave v = row bits 1-3, registers q = row bits 4-7 (16 rows x 8 planes).
 //
-// Phase 1 (A, one wave per 32-row group below mtrunc): load each row as one 1 KB wave
-// access (row-uniform, so the error-locator scaling reads its table from
-// SGPRs), scale into subfield coordinates, IFFT layer 0 in byte form (rows
-// 2i, 2i+1 of a lane are both in registers; wave-uniform tables), then
+// Phase 1 (A, one 16-row unit below mtrunc at a time): load each row as one
+// 1 KB wave access (row-uniform, so the error-locator scaling reads its table
+// from SGPRs), scale into subfield coordinates, IFFT layer 0 in byte form
+// (rows 2i, 2i+1 of a lane are both in registers; wave-uniform tables), then
 // permlane32 / permlane16 swaps and an in-lane bit transpose into planes, and
-// IFFT layers 1-4 as constant XOR networks (one code path per wave role).
-// Phase 2 (B, waves 0-7, one code path): IFFT layers 5-7, the formal
-// derivative, FFT layers 7-5.  The derivative D = I + sum_b N_b (N_b: row r
+// IFFT layers 1-3 as constant XOR networks (the unit's code path chosen per
+// butterfly).
+// Phase 2 (B, waves 0-7, one code path): IFFT layers 4-7, the formal
+// derivative, FFT layers 7-4.  The derivative D = I + sum_b N_b (N_b: row r
 // gets in[r | 2^b] when bit b of r is clear) splits into H = N_4..N_7, local
 // in B, and Lo = N_0..N_3, which acts on row bits the B layers neither touch
 // nor read their twiddles from, so it commutes with them:
@@ -41,9 +42,9 @@
 // since the FFT layers invert the IFFT layers (same twiddles, inverse
 // butterflies).  Lo u needs rows of other waves: they come from the LDS image
 // of u, which phase 2 still holds.
-// Phase 3 (A, one wave per group with a revealed row): FFT layers 4-1 (constant networks,
-// pruned by the revealed-row mask), back to bytes, FFT layer 0 in byte form,
-// reveal (error-locator scaling out of subfield coordinates), 1 KB stores.
+// Phase 3 (A, one 16-row unit with a revealed row at a time): FFT layers 3-1
+// (constant networks), back to bytes, FFT layer 0 in byte form, reveal
+// (error-locator scaling out of subfield coordinates), 1 KB stores.
 //
 // The LDS image holds rows < 160 (1 KB each): the kernel serves n = 256 codecs
 // with m + k <= 160 (C4: 160).  Rows >= mtrunc of the decoder IFFT input are
@@ -181,13 +182,42 @@ constexpr uint32_t z_after(uint32_t z, int qb) {
 // it touches in SGPRs for the whole loop (hundreds of SGPR spills).
 typedef __attribute__((address_space(4))) const RecArgs cargs_t;
 
+// RS_DEC_ABL: bitmask of steps left out (build experiments only; wrong results):
+// 1 row loads, 2 phase-1 transform, 4 phase 2, 8 phase-3 transform, 16 reveal
+#ifndef RS_DEC_ABL
+#define RS_DEC_ABL 0
+#endif
+#define ABL(b) ((RS_DEC_ABL >> (b)) & 1)
+// RS_DEC_STAMP (diagnostic builds only): per-wave cycle sums of the loop's
+// segments, written to DecPlan::stamps and printed by the launcher.
+#ifdef RS_DEC_STAMP
+#define STAMP(k)                                          \
+    do {                                                  \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+        seg[k] += now_ - last_;                           \
+        last_ = now_;                                     \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+[[maybe_unused]] constexpr int kSegs = 16;
+// Where an early wave passes phase 2's barriers inside its first phase-1
+// unit: 1 after the scaling, 2 after IFFT layer 0, 3 after the transpose.
+#ifndef RS_DEC_EARLY_BAR
+#define RS_DEC_EARLY_BAR 2
+#endif
+
 template <bool STRIDED>
 struct Dec {
     cargs_t *ap;        // the kernel's RecArgs (first kernel argument, kernarg offset 0)
-    uint32_t V[16][8];  // A layout: V[i] = row 32w + 2i + z (byte form: row 32w + t at V[t >> 1][4 (t & 1) ..])
+    // A layout: V[i] (i < 8) = row 16u + 2i + z of the unit being worked on
+    // (byte form: row 16u + t at V[t >> 1][4 (t & 1) ..]); V[8..15] park a
+    // second unit.  B layout (phase 2): V[q] = row z + 2v + 16q.
+    uint32_t V[16][8];
     int w;
     uint32_t lds0;      // LDS address of the image
-    int grp;            // phase 1 / phase 3 row group: rows 32 grp .. 32 grp + 31 (A layout)
     uint64_t col;       // first column byte of the tile
     uint8_t *sbase;     // this stripe (strided shards), or nullptr
 
@@ -243,15 +273,15 @@ struct Dec {
         return (l & 15u) * 64u + (l >> 5) * 32u + ((l >> 4) & 1u) * 16u;
     }
 
-    // ---------------- phase 1: rows 32 grp .. 32 grp + 31
-    // all 32 row loads in flight at once, straight into the row registers
-    // (the wave's 32 KB; missing rows read as zero through an empty range)
-    __device__ __forceinline__ void load_rows() {
+    // ---------------- phase 1: rows 16 u .. 16 u + 15 into V[0..7]
+    // all 16 row loads in flight at once, straight into the row registers
+    // (missing rows read as zero through an empty range)
+    __device__ __forceinline__ void load_rows(int u) {
         cargs_t &a = args();
         const uint32_t off = lane_off();
-        sfor<32>([&](auto T) __attribute__((always_inline)) {
+        sfor<16>([&](auto T) __attribute__((always_inline)) {
             constexpr int t = decltype(T)::value;
-            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(src_rsrc(a, 32 * grp + t), off, 0, 0);
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(src_rsrc(a, 16 * u + t), off, 0, 0);
 #pragma unroll
             for (int d = 0; d < 4; d++) V[t >> 1][4 * (t & 1) + d] = x[d];
         });
@@ -259,15 +289,15 @@ struct Dec {
     }
     // Rows into subfield coordinates, each times its errLocs factor: row t's
     // table is loaded while row t - 1 is multiplied (one table in flight; all
-    // 32 at once would not fit the SGPRs).
-    __device__ __forceinline__ void scale() {
+    // 16 at once would not fit the SGPRs).
+    __device__ __forceinline__ void scale(int u) {
         cargs_t &a = args();
-        cu32_t *base = ctab(a.tw_in) + (uint64_t)(32 * grp) * kTw16;
+        cu32_t *base = ctab(a.tw_in) + (uint64_t)(16 * u) * kTw16;
         Tab<20> cur = tab_at<20>(base);
-        sfor<32>([&](auto T) __attribute__((always_inline)) {
+        sfor<16>([&](auto T) __attribute__((always_inline)) {
             constexpr int t = decltype(T)::value;
             Tab<20> nxt;
-            if constexpr (t + 1 < 32) nxt = tab_at<20>(base + (t + 1) * kTw16);
+            if constexpr (t + 1 < 16) nxt = tab_at<20>(base + (t + 1) * kTw16);
             uint32_t(&v)[8] = V[t >> 1];
             constexpr int o = 4 * (t & 1);
             // pair each lane's lo bytes with the hi bytes of the same symbols:
@@ -281,34 +311,34 @@ struct Dec {
             asm volatile("" : "+v"(s[0]), "+v"(s[1]), "+v"(s[2]), "+v"(s[3]));
 #pragma unroll
             for (int d = 0; d < 4; d++) v[o + d] = s[d];
-            if constexpr (t + 1 < 32) cur = nxt;
+            if constexpr (t + 1 < 16) cur = nxt;
             __builtin_amdgcn_sched_barrier(0);
         });
     }
     // IFFT layer 0 (rows 2i, 2i + 1) in byte form: y ^= x; x ^= y * t
     // (pair i + 1's table loads while pair i multiplies)
-    __device__ __forceinline__ void ifft0_bytes() {
+    __device__ __forceinline__ void ifft0_bytes(int u) {
         cargs_t &a = args();
-        cu32_t *tw = ctab(a.tw_ifft) + (uint64_t)slot0(32 * grp) * kTw8;  // slot0(32w + 2i) = slot0(32w) + slot0(2i)
+        cu32_t *tw = ctab(a.tw_ifft) + (uint64_t)slot0(16 * u) * kTw8;  // slot0(16u + 2i) = slot0(16u) + slot0(2i)
         Tab<5> cur = tab_at<5>(tw);
-        sfor<16>([&](auto I) __attribute__((always_inline)) {
+        sfor<8>([&](auto I) __attribute__((always_inline)) {
             constexpr int i = decltype(I)::value;
             Tab<5> nxt;
-            if constexpr (i + 1 < 16) nxt = tab_at<5>(tw + slot0(2 * i + 2) * kTw8);
+            if constexpr (i + 1 < 8) nxt = tab_at<5>(tw + slot0(2 * i + 2) * kTw8);
             uint32_t *x = bytes(2 * i), *y = bytes(2 * i + 1);
 #pragma unroll
             for (int d = 0; d < 4; d++) y[d] ^= x[d];
             mul8_add(x, y, cur);
             asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]));
-            if constexpr (i + 1 < 16) cur = nxt;
+            if constexpr (i + 1 < 8) cur = nxt;
             __builtin_amdgcn_sched_barrier(0);
         });
     }
     // FFT layer 0 in byte form: x ^= y * t; y ^= x (pairs with a revealed row)
-    __device__ __forceinline__ void fft0_bytes(uint32_t nw) {
+    __device__ __forceinline__ void fft0_bytes(int u, uint32_t nw) {
         cargs_t &a = args();
-        cu32_t *tw = ctab(a.tw_fft) + (uint64_t)(kFft0Slot + slot0(32 * grp)) * kTw8;
-        sfor<16>([&](auto I) __attribute__((always_inline)) {
+        cu32_t *tw = ctab(a.tw_fft) + (uint64_t)(kFft0Slot + slot0(16 * u)) * kTw8;
+        sfor<8>([&](auto I) __attribute__((always_inline)) {
             constexpr int i = decltype(I)::value;
             if ((nw >> (2 * i)) & 3u) {
                 uint32_t *x = bytes(2 * i), *y = bytes(2 * i + 1);
@@ -323,7 +353,7 @@ struct Dec {
     // mask: register rows to convert (bit i)
     __device__ __forceinline__ void to_planes(uint32_t mask) {
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
+        for (int i = 0; i < 8; i++) {
             if (!((mask >> i) & 1)) continue;
             // lane bit 5: symbol group p <-> row bit 0
 #pragma unroll
@@ -339,7 +369,7 @@ struct Dec {
     }
     __device__ __forceinline__ void to_bytes(uint32_t mask) {
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
+        for (int i = 0; i < 8; i++) {
             if (!((mask >> i) & 1)) continue;
             bs_transpose8(V[i]);
             swap16(V[i][0], V[i][2]);
@@ -351,30 +381,19 @@ struct Dec {
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    // IFFT layers 1-4 of role W (rows 32 W ..): register rows i, i + 2^(L-1) (row bit L)
-    template <int W>
-    __device__ __forceinline__ void ifft_a() {
-        sfor<4>([&](auto LI) __attribute__((always_inline)) {
-            constexpr int L = 1 + decltype(LI)::value, s = 1 << (L - 1);
-            sfor<8>([&](auto Q) __attribute__((always_inline)) {
-                constexpr int q = decltype(Q)::value;
-                constexpr int i = ((q >> (L - 1)) << L) | (q & (s - 1));
-                bs_ifft2<L, ((32 * W + 2 * i) >> (L + 1))>(V[i], V[i + s]);
-            });
-        });
-    }
-    // IFFT layers 1-4 with the role grp chosen per butterfly: V is live into
-    // the role choice here, and a branch per role around the whole pass left
-    // the allocator holding two copies of the rows.  Each role writes
-    // x ^ M y into fresh registers (no tied operands) and the result moves into x.
+    // IFFT butterfly of layer L (1-3) on register rows I, I + 2^(L-1), the
+    // unit's twiddle chosen per butterfly: V is live into the choice here, and
+    // a branch per unit around the whole pass left the allocator holding two
+    // copies of the rows.  Each branch writes x ^ M y into fresh registers (no
+    // tied operands) and the result moves into x.
     template <int L, int I>
-    __device__ __forceinline__ void ifft_bf_a() {
+    __device__ __forceinline__ void ifft_bf_a(int u) {
         constexpr int s = 1 << (L - 1);
         Half &x = V[I], &y = V[I + s];
         xor8(y, x);
         Half nx;
-        dispatch<5>(grp, [&](auto W) __attribute__((always_inline)) {
-            constexpr int g = (32 * decltype(W)::value + 2 * I) >> (L + 1);
+        dispatch<kImgRows / 16>(u, [&](auto U) __attribute__((always_inline)) {
+            constexpr int g = (16 * decltype(U)::value + 2 * I) >> (L + 1);
             sfor<8>([&](auto K) __attribute__((always_inline)) {
                 constexpr int k = decltype(K)::value;
                 xor_net8f<DT::m8[L][g][k]>(nx[k], x[k], y);
@@ -384,15 +403,14 @@ struct Dec {
         for (int k = 0; k < 8; k++) x[k] = nx[k];
         __builtin_amdgcn_sched_barrier(0);
     }
-    // FFT butterfly of layer L (1-4) on register rows I, I + 2^(L-1), the role
-    // grp chosen per butterfly as in ifft_bf_a: x ^= M y; y ^= x
+    // FFT butterfly of layer L (1-3) on register rows I, I + 2^(L-1): x ^= M y; y ^= x
     template <int L, int I>
-    __device__ __forceinline__ void fft_bf_a() {
+    __device__ __forceinline__ void fft_bf_a(int u) {
         constexpr int s = 1 << (L - 1);
         Half &x = V[I], &y = V[I + s];
         Half nx;
-        dispatch<5>(grp, [&](auto W) __attribute__((always_inline)) {
-            constexpr int g = (32 * decltype(W)::value + 2 * I) >> (L + 1);
+        dispatch<kImgRows / 16>(u, [&](auto U) __attribute__((always_inline)) {
+            constexpr int g = (16 * decltype(U)::value + 2 * I) >> (L + 1);
             sfor<8>([&](auto K) __attribute__((always_inline)) {
                 constexpr int k = decltype(K)::value;
                 xor_net8f<DT::m8[L][g][k]>(nx[k], x[k], y);
@@ -403,23 +421,60 @@ struct Dec {
         xor8(y, x);
         __builtin_amdgcn_sched_barrier(0);
     }
-    __device__ __forceinline__ void fft_a_rt() {
-        sfor<4>([&](auto LI) __attribute__((always_inline)) {
-            constexpr int L = 4 - decltype(LI)::value, s = 1 << (L - 1);
-            sfor<8>([&](auto Q) __attribute__((always_inline)) {
+    __device__ __forceinline__ void fft_a(int u) {
+        sfor<3>([&](auto LI) __attribute__((always_inline)) {
+            constexpr int L = 3 - decltype(LI)::value, s = 1 << (L - 1);
+            sfor<4>([&](auto Q) __attribute__((always_inline)) {
                 constexpr int q = decltype(Q)::value;
-                fft_bf_a<L, ((q >> (L - 1)) << L) | (q & (s - 1))>();
+                fft_bf_a<L, ((q >> (L - 1)) << L) | (q & (s - 1))>(u);
             });
         });
     }
-    __device__ __forceinline__ void ifft_a_rt() {
-        sfor<4>([&](auto LI) __attribute__((always_inline)) {
+    __device__ __forceinline__ void ifft_a(int u) {
+        sfor<3>([&](auto LI) __attribute__((always_inline)) {
             constexpr int L = 1 + decltype(LI)::value, s = 1 << (L - 1);
-            sfor<8>([&](auto Q) __attribute__((always_inline)) {
+            sfor<4>([&](auto Q) __attribute__((always_inline)) {
                 constexpr int q = decltype(Q)::value;
-                ifft_bf_a<L, ((q >> (L - 1)) << L) | (q & (s - 1))>();
+                ifft_bf_a<L, ((q >> (L - 1)) << L) | (q & (s - 1))>(u);
             });
         });
+    }
+    // the phase-1 transform of unit u, from its rows in HBM (loads already
+    // issued when `loaded`) to planes in V[0..7]
+    // nbar: workgroup barriers to pass after the scaling (an early wave passes
+    // phase 2's two barriers there, so it does not hold phase 2 back)
+    __device__ __forceinline__ void phase1(int u, bool loaded, int nbar = 0) {
+        if (16 * u >= args().mtrunc) {  // rows past mtrunc: zero (the image rows still have to be written)
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) V[i][k] = 0;
+            for (int b = 0; b < nbar; b++) lds_barrier();
+            return;
+        }
+        if (!loaded)
+            if constexpr (!ABL(0)) load_rows(u);
+        scale(u);
+        if (RS_DEC_EARLY_BAR == 1)
+            for (int b = 0; b < nbar; b++) lds_barrier();
+        if constexpr (!ABL(1)) ifft0_bytes(u);
+        if (RS_DEC_EARLY_BAR == 2)
+            for (int b = 0; b < nbar; b++) lds_barrier();
+        to_planes(0xFFu);
+        if (RS_DEC_EARLY_BAR == 3)
+            for (int b = 0; b < nbar; b++) lds_barrier();
+        if constexpr (!ABL(1)) ifft_a(u);
+    }
+    // V[0..7] <-> V[8..15] (the parked unit)
+    __device__ __forceinline__ void park_swap() {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t t = V[i][k];
+                V[i][k] = V[8 + i][k];
+                V[8 + i][k] = t;
+            }
     }
     // ---------------- LDS image: row r at r * 1024, plane quad pq at + pq * 512, lane at + (lane & 31) * 16
     __device__ __forceinline__ void img_put(int row_nz, const Half &v) {  // row_nz: row without the lane's z
@@ -437,6 +492,17 @@ struct Dec {
         const u32x4 y = *(const lds_u4 *)(uintptr_t)(o + 512);
         v[0] = x[0], v[1] = x[1], v[2] = x[2], v[3] = x[3];
         v[4] = y[0], v[5] = y[1], v[6] = y[2], v[7] = y[3];
+    }
+    // unit u's 8 register rows from / to V[RO..RO+7]
+    template <int RO>
+    __device__ __forceinline__ void unit_put(int u) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) img_put(16 * u + 2 * i, V[RO + i]);
+    }
+    template <int RO>
+    __device__ __forceinline__ void unit_get(int u) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) img_get(16 * u + 2 * i, V[RO + i]);
     }
     // v ^= image row row_nz (+ the lane's z); ONLY_Z0: v ^= image row `row_nz`
     // itself in lanes with z = 0 (zmask all ones there), nothing in z = 1 lanes
@@ -465,23 +531,26 @@ struct Dec {
 #pragma unroll
                 for (int k = 0; k < 8; k++) V[q][k] = 0;
         }
-        // IFFT layers 5, 6, 7 (row bits 5-7 = q bits 1-3); rows q >= NQ start at zero
+        // IFFT layers 4-7 (row bits 4-7 = q bits 0-3); rows q >= NQ start at zero
         constexpr uint32_t Z0 = ~((1u << NQ) - 1u) & 0xFFFFu;
-        ifft_b<5, Z0>();
-        constexpr uint32_t Z1 = z_after(Z0, 1);
-        ifft_b<6, Z1>();
-        constexpr uint32_t Z2 = z_after(Z1, 2);
-        ifft_b<7, Z2>();
+        ifft_b<4, Z0>();
+        constexpr uint32_t Z1 = z_after(Z0, 0);
+        ifft_b<5, Z1>();
+        constexpr uint32_t Z2 = z_after(Z1, 1);
+        ifft_b<6, Z2>();
+        constexpr uint32_t Z3 = z_after(Z2, 2);
+        ifft_b<7, Z3>();
         // (I + H): out[q] ^= in[q | 2^b] for clear bits b of q (row bits 4-7); ascending q reads unmodified partners
 #pragma unroll
         for (int q = 0; q < 16; q++)
 #pragma unroll
             for (int b = 0; b < 4; b++)
                 if (!((q >> b) & 1)) xor8(V[q], V[q | (1 << b)]);
-        // FFT layers 7, 6, 5; outputs only rows q < NQ
+        // FFT layers 7-4; outputs only rows q < NQ
         fft_b<7, 0xFFFFu>();
-        fft_b<6, 0x0FFFu>();  // layer 5 reads rows 0..11
-        fft_b<5, (1u << NQ) - 1u>();
+        fft_b<6, 0x0FFFu>();         // layer 5 reads rows 0..11
+        fft_b<5, (1u << NQ) - 1u>();  // layer 4 reads rows 0..9
+        fft_b<4, (1u << NQ) - 1u>();
         // + Lo u: rows r | 2^b for clear bits b of r among row bits 0-3, read from the image of u
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
@@ -515,27 +584,55 @@ struct Dec {
         });
     }
 
-    // ---------------- phase 3 reveal: rows 32 grp + t revealed (nw), out = work * (mod - errLocs)
-    __device__ __forceinline__ void reveal(uint32_t nw) {
+    // ---------------- phase 3: FFT layers 3-0 and the reveal of unit u's rows (V[0..7])
+    // revealed rows of unit u (bit t: row 16u + t)
+    __device__ __forceinline__ static uint32_t unit_need(const Need &need, int u) {
+        uint32_t word = need.w[0];
+#pragma unroll
+        for (int k = 1; k < 8; k++) {
+            asm volatile("" : "+s"(word));  // a select chain, not a stack array (rec_common.hpp rows_needed)
+            word = (u >> 1) == k ? need.w[k] : word;
+        }
+        return (word >> (16 * (u & 1))) & 0xFFFFu;
+    }
+    __device__ __forceinline__ void phase3(int u) {
         cargs_t &a = args();
         const Need need = load_need(a.need);
-        // output index of revealed row r = 32 grp + t (rec_common.hpp reveal_index):
+        const uint32_t nw = __builtin_amdgcn_readfirstlane(unit_need(need, u));
+        if constexpr (!ABL(3)) fft_a(u);
+        uint32_t pairs = 0;  // register rows holding a revealed row (either z)
+#pragma unroll
+        for (int i = 0; i < 8; i++) pairs |= ((nw >> (2 * i)) & 3u) ? 1u << i : 0u;
+        to_bytes(pairs);
+        fft0_bytes(u, nw);
+        if constexpr (!ABL(4)) reveal(u, nw, need);
+    }
+    // out = work * (mod - errLocs) for the revealed rows 16u + t (bit t of nw)
+    __device__ __forceinline__ void reveal(int u, uint32_t nw, const Need &need) {
+        cargs_t &a = args();
+        // output index of revealed row r = 16 u + t (rec_common.hpp reveal_index):
         // its rank among the revealed rows in the rotated order [m, n), [0, m)
         int below = 0, below_m = 0, total = 0;
+        uint32_t word = need.w[0];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             const int c = __builtin_popcount(need.w[k]);
             total += c;
             if (k * 32 + 32 <= a.m) below_m += c;
             else if (k * 32 < a.m) below_m += __builtin_popcount(need.w[k] & ((1u << (a.m & 31)) - 1));
-            below += k < grp ? c : 0;
+            below += k < (u >> 1) ? c : 0;
+            if (k > 0) {
+                asm volatile("" : "+s"(word));
+                word = (u >> 1) == k ? need.w[k] : word;
+            }
         }
+        if (u & 1) below += __builtin_popcount(word & 0xFFFFu);
         const int j_hi = below - below_m, j_lo = total - below_m + below;
         const uint32_t off = lane_off();
-        sfor<32>([&](auto T) __attribute__((always_inline)) {
+        sfor<16>([&](auto T) __attribute__((always_inline)) {
             constexpr int t = decltype(T)::value;
             if ((nw >> t) & 1u) {
-                const int r = 32 * grp + t;
+                const int r = 16 * u + t;
                 const int j = (r >= a.m ? j_hi : j_lo) + __builtin_popcount(nw & ((1u << t) - 1u));
                 uint32_t o[4];
                 uint32_t y[4] = {bytes(t)[0], bytes(t)[1], bytes(t)[2], bytes(t)[3]};
@@ -549,65 +646,36 @@ struct Dec {
     }
 };
 
-// A role branch starts and ends with a volatile marker of its own: the
-// branches' first and last instructions (the image stores) are identical
-// across roles, and the CFG simplifier would otherwise sink them into a shared
-// block that has to merge every row value of every role.
-template <int W>
-__device__ __forceinline__ void role_mark() {
-    asm volatile("; role %0" ::"n"(W));
-}
-
-// RS_DEC_ABL: bitmask of steps left out (build experiments only; wrong results):
-// 1 row loads, 2 phase-1 transform, 4 phase 2, 8 phase-3 transform, 16 reveal
-#ifndef RS_DEC_ABL
-#define RS_DEC_ABL 0
-#endif
-#define ABL(b) ((RS_DEC_ABL >> (b)) & 1)
-// RS_DEC_STAMP (diagnostic builds only): per-wave cycle sums of the loop's
-// segments, written to DecPlan::stamps and printed by the launcher.
-#ifdef RS_DEC_STAMP
-#define STAMP(k)                                          \
-    do {                                                  \
-        const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
-        seg[k] += now_ - last_;                           \
-        last_ = now_;                                     \
-    } while (0)
-#else
-#define STAMP(k) \
-    do {         \
-    } while (0)
-#endif
-[[maybe_unused]] constexpr int kSegs = 16;
-
-// Waves per workgroup: 8 run phase 2 (B layout: wave = row bits 1-3); all of
-// them take phase-1 / phase-3 units.  12 = three waves per SIMD, one unit each.
+// Waves per workgroup: 8 run phase 2 (B layout: wave = row bits 1-3); waves
+// 8 .. kWaves-1 run phase 1 of the next tile meanwhile.  12 = three waves per SIMD.
 #ifndef RS_DEC_WAVES
 #define RS_DEC_WAVES 12
 #endif
 constexpr int kWaves = RS_DEC_WAVES;
-static_assert(kWaves >= 8 && kWaves <= 12, "wave count");
+static_assert(kWaves > 8 && kWaves <= 12, "wave count");
+constexpr int kUnits = kImgRows / 16;  // 16-row units below the image end
 
 // Work plan of a workgroup's waves (host-made, the same for every tile:
-// launch_rec_bs256).  Phase 1 (load, scale, IFFT layers 0-4 of a 32-row group)
-// and phase 3 (FFT layers 4-0 and reveal of a group with revealed rows) run
-// only on the groups below mtrunc, 5 at C4; each is a unit of one wave.  The
-// units go to waves so that the four SIMDs carry about the same VALU work
-// (wave w runs on SIMD w & 3), and phase 3 of tile t overlaps phase 1 of the
-// next tile, whose row loads the phase-1-only waves issue early.
+// launch_rec_bs256).  Phase 1 (load, scale, IFFT layers 0-3 of a 16-row unit)
+// runs on the units below mtrunc (10 at C4) and phase 3 (FFT layers 3-0 and
+// reveal) on the units with a revealed row.  Per wave, four 4-bit fields
+// (unit + 1, 0: none): phase-3 units 0 and 1, phase-1 units 0 and 1.  Waves
+// >= 8 hold phase-1 units only and run them before phase 2 of the previous
+// tile ("early"); waves < 8 run theirs after phase 3.
 struct DecPlan {
-    uint64_t p3;   // 4 bits per wave: phase-3 group + 1 (0: none)
-    uint64_t p1;   // 5 bits per wave: mask of phase-1 groups
-    int ntx;       // column tiles per stripe
-    int ntiles;    // column tiles x stripes
+    uint64_t code[3];  // 16 bits per wave, waves 4j .. 4j+3 in code[j]
+    int ntx;           // column tiles per stripe
+    int ntiles;        // column tiles x stripes
     uint64_t *stamps;  // RS_DEC_STAMP builds: kSegs cycle sums per wave
 };
 
 // Persistent over tiles t = blockIdx.x + i * gridDim.x (column tile t % ntx of
 // stripe t / ntx).  Iteration i runs phases 2 and 3 of tile t_(i-1) and phase
 // 1 of tile t_i:
-//   phase 2 (all waves) -> Y into the image -> phase-3 waves read their rows ->
-//   barrier (image free) -> phase 3 of t_(i-1) || phase 1 of t_i into the image.
+//   early phase 1 of t_i (waves >= 8, registers only) || phase 2 of t_(i-1)
+//   (waves < 8) -> Y into the image -> phase-3 waves read their rows ->
+//   barrier (image free) -> early units into the image; phase 3 of t_(i-1);
+//   late phase-1 units of t_i -> barrier (u of t_i in the image).
 template <bool STRIDED>
 __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a, DecPlan pl) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kImgRows * kTile / 4];
@@ -616,16 +684,11 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
     d.lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)lds;
     d.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int w = d.w;
-    const int p3g = (int)((pl.p3 >> (4 * w)) & 15u) - 1;
-    const uint32_t p1m = (uint32_t)(pl.p1 >> (5 * w)) & 31u;
-    const int first = p1m ? __builtin_ctz(p1m) : -1;
-    uint32_t nw = 0;  // revealed rows of the phase-3 group
-    if (p3g >= 0) {
-        const Need need = load_need(a.need);
-        nw = need.w[0];
-#pragma unroll
-        for (int k = 1; k < 8; k++) nw = p3g == k ? need.w[k] : nw;  // wave-uniform word select
-    }
+    const uint64_t cw = w < 4 ? pl.code[0] : w < 8 ? pl.code[1] : pl.code[2];
+    const uint32_t code = (uint32_t)(cw >> (16 * (w & 3))) & 0xFFFFu;
+    const int u3a = (int)(code & 15u) - 1, u3b = (int)((code >> 4) & 15u) - 1;
+    const int u1a = (int)((code >> 8) & 15u) - 1, u1b = (int)((code >> 12) & 15u) - 1;
+    const bool early = w >= 8;
     auto set_tile = [&](int t) {
         const int y = t / pl.ntx;
         d.col = (uint64_t)(t - y * pl.ntx) * kTile;
@@ -644,93 +707,66 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
 #endif
     for (;;) {
         const bool cur = t >= 0, more = tn < pl.ntiles;
+        const bool early_p1 = early && more && u1a >= 0;  // passes phase 2's barriers inside its first unit
+        if (early_p1) {
+            // ---- early phase 1 of tile tn (registers only); a first unit parks in V[8..15]
+            set_tile(tn);
+            const int n1 = u1b >= 0 ? 2 : 1;
+            // (loading unit b's rows into V[8..15] up front measured slower:
+            // 1950 vs 1694 us per 16 C4 stripes)
+#pragma nounroll
+            for (int s = 0; s < n1; s++) {  // one copy of the phase-1 code
+                if (s) d.park_swap();
+                d.phase1(s ? u1b : u1a, false, s == 0 && cur ? 2 : 0);
+            }
+        }
+        STAMP(12);
         if (cur) {
             // ---- phase 2: Y = B_F (I + H) B_I u + Lo u (B layout)
-            if (w < 8)
+            if (!early)
                 if constexpr (!ABL(2)) d.phase2();
             STAMP(0);
-            lds_barrier();  // every wave has read u
+            if (!early_p1) lds_barrier();  // every wave has read u
             STAMP(1);
-            if (w < 8) {
+            if (!early) {
                 int wt = w;
                 asm volatile("" : "+s"(wt));
 #pragma unroll
                 for (int q = 0; q < Dec<STRIDED>::NQ; q++) d.img_put(2 * wt + 16 * q, d.V[q]);
             }
-            lds_barrier();
+            if (!early_p1) lds_barrier();  // Y is in the image
             STAMP(2);
-        }
-        const bool early = more && first >= 0 && (p3g < 0 || !cur);
-        if (early) {  // a phase-1-only wave: its first group's rows are on the way during the exchange
-            set_tile(tn);
-            d.grp = first;
-            if constexpr (!ABL(0)) d.load_rows();
-        }
-        if (cur) {
-            if (p3g >= 0) {
-                int g = p3g;
-                asm volatile("" : "+s"(g));
-                d.grp = g;
-#pragma unroll
-                for (int i = 0; i < 16; i++) d.img_get(32 * g + 2 * i, d.V[i]);
-            }
-            lds_barrier();  // the image is free for phase 1 of the next tile
-            STAMP(3);
-            // ---- phase 3: FFT layers 4-0 and reveal of the revealed rows of group p3g
-            if (p3g >= 0) {
+            if (u3a >= 0) {
+                // ---- phase 3 of tile t, one unit at a time (each read from the
+                // image before the barrier below frees it)
                 set_tile(t);
-                if constexpr (!ABL(3)) d.fft_a_rt();
-                STAMP(13);
-                // opaque per tile: the loop-invariant row tests would otherwise be
-                // hoisted out of the tile loop as 48 live 64-bit masks (SGPR spills)
-                uint32_t nwt = nw;
-                asm volatile("" : "+s"(nwt));
-                uint32_t pairs = 0;  // register rows holding a revealed row (either z)
-#pragma unroll
-                for (int i = 0; i < 16; i++) pairs |= ((nwt >> (2 * i)) & 3u) ? 1u << i : 0u;
-                d.to_bytes(pairs);
-                d.fft0_bytes(nwt);
-                STAMP(14);
-                if constexpr (!ABL(4)) d.reveal(nwt);
+                const int n3 = u3b >= 0 ? 2 : 1;
+#pragma nounroll
+                for (int s = 0; s < n3; s++) {
+                    const int u = s ? u3b : u3a;
+                    d.template unit_get<0>(u);
+                    d.phase3(u);
+                }
             }
             STAMP(4);
         }
-        if (more) {
-            // ---- phase 1: u = IFFT layers 0-4 of the scaled rows (A layout), into the image
+        if (!early && more && u1a >= 0) {
+            // ---- late phase 1 of tile tn (registers only)
             set_tile(tn);
-            for (uint32_t m = p1m; m; m &= m - 1) {
-                const int g = __builtin_ctz(m);
-                d.grp = g;
-                if (!(early && g == first))
-                    if constexpr (!ABL(0)) d.load_rows();
-                STAMP(7);
-                d.scale();
-                STAMP(8);
-                if constexpr (!ABL(1)) d.ifft0_bytes();
-                STAMP(9);
-                d.to_planes(0xFFFFu);
-                STAMP(10);
-                // one code path per role: the rows leave for the image inside
-                // it, so no row value is merged from the role branches
-#ifdef RS_DEC_ROLE_PASS
-                dispatch<5>(g, [&](auto W) __attribute__((always_inline)) {
-                    constexpr int gw = decltype(W)::value;
-                    role_mark<gw>();
-                    if constexpr (!ABL(1)) d.template ifft_a<gw>();
-#pragma unroll
-                    for (int i = 0; i < 16; i++) d.img_put(32 * gw + 2 * i, d.V[i]);
-                    role_mark<gw>();
-                });
-#else
-                if constexpr (!ABL(1)) d.ifft_a_rt();
-#pragma unroll
-                for (int i = 0; i < 16; i++) d.img_put(32 * g + 2 * i, d.V[i]);
-#endif
-                STAMP(12);
-            }
+            d.phase1(u1a, false);
         }
         STAMP(5);
         if (!more) break;
+        lds_barrier();  // the image is free for phase 1 of tile tn
+        STAMP(3);
+        if (u1a >= 0) {
+            if (early) {
+                d.template unit_put<0>(u1b >= 0 ? u1b : u1a);
+                if (u1b >= 0) d.template unit_put<8>(u1a);
+            } else {
+                d.template unit_put<0>(u1a);
+            }
+        }
         lds_barrier();  // u of tile tn is in the image
         STAMP(6);
         t = tn;
@@ -742,89 +778,60 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
 #endif
 }
 
-// Unit placement (see DecPlan).  Costs in VALU work: a phase-3 unit 2, a
-// phase-1 unit 4 (load, scale and byte-form layer 0 of 32 rows on top of
-// the plane layers).  A wave runs its units one after the other; wave w runs
-// on SIMD w & 3.  Alone on its SIMD a wave issues a VALU instruction every
-// ~4.3 cycles; SIMDs shared by two / three waves issue one every ~3.15 / ~2.8
-// cycles between them (scripts/micro/valu_rate.hip).  The plan minimises
-// max(chain x 4.3, SIMD load x 3.0) over every placement with at most one
-// phase-3 unit per wave (it is read from the image before phase 1 of the
-// next tile may overwrite it), and one unit per wave when there are enough
-// waves; searched once per (groups, revealed groups) and cached.
+// Unit placement (see DecPlan).  VALU cost: a phase-1 unit 2, a phase-3 unit
+// 1; phase 2 and the exchange cost the waves < 8 about 2 before their phase 3
+// / late phase 1 starts, while the early waves' phase-1 units overlap it.  So
+// the early waves take two phase-1 units each first, the rest of phase 1 goes
+// one unit per wave to waves < 8 from the top (7, 6, ...), and the phase-3
+// units go round-robin, at most two per wave (run one after the other), to
+// the waves < 8 without phase 1: about 4 per wave everywhere at C4.
+// Wave w runs on SIMD w & 3: waves 8-11 land one per SIMD.
 DecPlan make_plan(const RecArgs &a) {
-    const int G = (a.mtrunc + 31) / 32;
-    uint32_t rmask = 0;  // groups with revealed rows
-    for (int g = 0; g < G; g++)
-        if (a.need[g]) rmask |= 1u << g;
+    // phase 1 writes every image row: units past mtrunc write zeros (Dec::phase1)
+    const int G = kUnits;
+    uint32_t rmask = 0;  // units with revealed rows
+    for (int u = 0; u < G; u++)
+        if ((a.need[u >> 1] >> (16 * (u & 1))) & 0xFFFFu) rmask |= 1u << u;
     static std::mutex mu;
     static std::map<uint32_t, DecPlan> cache;
-    const uint32_t key = (uint32_t)G << 8 | rmask;
+    const uint32_t key = (uint32_t)G << 16 | rmask;
     {
         std::lock_guard<std::mutex> lk(mu);
         auto it = cache.find(key);
         if (it != cache.end()) return it->second;
     }
-    int r3[5], n3 = 0;
-    for (int g = 0; g < G; g++)
-        if ((rmask >> g) & 1) r3[n3++] = g;
-    constexpr int C3 = 2, C1 = 4;
-    double best = 1e30;
+    int u1[kWaves][2], u3[kWaves][2];
+    for (int w = 0; w < kWaves; w++) u1[w][0] = u1[w][1] = u3[w][0] = u3[w][1] = -1;
+    const int ne = kWaves - 8;
+    int u = 0;
+    for (int s = 0; s < 2; s++)
+        for (int e = 0; e < ne && u < G; e++) u1[8 + e][s] = u++;
+    for (int w = 7; w >= 0 && u < G; w--) u1[w][0] = u++;
+    if (u < G) {  // more units than the plan can hold: the launcher falls back
+        DecPlan bad{};
+        bad.ntiles = -1;
+        return bad;
+    }
+    int free3[8], nf = 0;
+    for (int w = 0; w < 8; w++)
+        if (u1[w][0] < 0) free3[nf++] = w;
+    int j = 0;
+    for (int g = 0; g < G; g++) {
+        if (!((rmask >> g) & 1)) continue;
+        const int w = free3[j % nf], s = j / nf;
+        if (s > 1) {
+            DecPlan bad{};
+            bad.ntiles = -1;
+            return bad;
+        }
+        u3[w][s] = g;
+        j++;
+    }
     DecPlan bp{};
-    auto score = [&](const int *load) {
-        double sc = 0;
-        for (int w = 0; w < kWaves; w++) sc = std::max(sc, load[w] * 4.3);
-        for (int q = 0; q < 4; q++) {
-            int sl = 0;
-            for (int w = q; w < kWaves; w += 4) sl += load[w];
-            sc = std::max(sc, sl * 3.0);
-        }
-        return sc;
-    };
-    const bool one_each = n3 + G <= kWaves;
-    for (uint32_t s3 = 0; s3 < (1u << kWaves); s3++) {
-        if (__builtin_popcount(s3) != n3) continue;
-        if (one_each) {
-            const uint32_t comp = ((1u << kWaves) - 1) & ~s3;
-            for (uint32_t s1 = comp;; s1 = (s1 - 1) & comp) {  // phase-1 waves: G of the others
-                if (!s1) break;
-                if (__builtin_popcount(s1) != G) continue;
-                int load[kWaves] = {0};
-                for (int w = 0; w < kWaves; w++) load[w] = ((s3 >> w) & 1) * C3 + ((s1 >> w) & 1) * C1;
-                const double sc = score(load);
-                if (sc < best - 1e-9) {
-                    best = sc;
-                    bp = DecPlan{};
-                    int j = 0, g = 0;
-                    for (int w = 0; w < kWaves; w++) {
-                        if ((s3 >> w) & 1) bp.p3 |= (uint64_t)(r3[j++] + 1) << (4 * w);
-                        if ((s1 >> w) & 1) bp.p1 |= 1ull << (5 * w + g++);
-                    }
-                }
-            }
-            continue;
-        }
-        int w1[5] = {0, 0, 0, 0, 0};
-        for (;;) {  // non-decreasing wave indices w1[0..G-1]
-            int load[kWaves] = {0};
-            for (int w = 0; w < kWaves; w++)
-                if ((s3 >> w) & 1) load[w] += C3;
-            for (int g = 0; g < G; g++) load[w1[g]] += C1;
-            const double sc = score(load);
-            if (sc < best - 1e-9) {
-                best = sc;
-                bp = DecPlan{};
-                int j = 0;
-                for (int w = 0; w < kWaves; w++)
-                    if ((s3 >> w) & 1) bp.p3 |= (uint64_t)(r3[j++] + 1) << (4 * w);
-                for (int g = 0; g < G; g++) bp.p1 |= 1ull << (5 * w1[g] + g);
-            }
-            int g = G - 1;
-            while (g >= 0 && w1[g] == kWaves - 1) g--;
-            if (g < 0) break;
-            w1[g]++;
-            for (int h = g + 1; h < G; h++) w1[h] = w1[g];
-        }
+    for (int w = 0; w < kWaves; w++) {
+        const uint64_t c = (uint64_t)(u3[w][0] + 1) | (uint64_t)(u3[w][1] + 1) << 4 | (uint64_t)(u1[w][0] + 1) << 8 |
+                           (uint64_t)(u1[w][1] + 1) << 12;
+        bp.code[w >> 2] |= c << (16 * (w & 3));
     }
     std::lock_guard<std::mutex> lk(mu);
     cache[key] = bp;
@@ -850,6 +857,7 @@ hipError_t launch_rec_bs256(const RecArgs &a, hipStream_t s) {
         if (dev < 64) cus_of[dev].store(cus);
     }
     DecPlan pl = make_plan(a);
+    if (pl.ntiles < 0) return hipErrorNotSupported;  // cannot happen for mtrunc <= kImgRows
     pl.ntx = (int)((a.S + kTile - 1) / kTile);
     const uint64_t ny = a.base && a.nstripes > 1 ? (uint64_t)a.nstripes : 1;
     if ((uint64_t)pl.ntx * ny > (uint64_t)INT32_MAX) return hipErrorInvalidValue;
@@ -871,8 +879,9 @@ hipError_t launch_rec_bs256(const RecArgs &a, hipStream_t s) {
         std::vector<uint64_t> h(nst);
         (void)hipStreamSynchronize(s);
         (void)hipMemcpy(h.data(), dstamps, nst * sizeof(uint64_t), hipMemcpyDeviceToHost);
-        std::fprintf(stderr, "stamps: grid %u tiles %d plan p3 %012llx p1 %015llx (mean cycles per workgroup)\n", grid,
-                     pl.ntiles, (unsigned long long)pl.p3, (unsigned long long)pl.p1);
+        std::fprintf(stderr, "stamps: grid %u tiles %d plan %016llx %016llx %016llx (mean cycles per workgroup)\n", grid,
+                     pl.ntiles, (unsigned long long)pl.code[0], (unsigned long long)pl.code[1],
+                     (unsigned long long)pl.code[2]);
         for (int w = 0; w < kWaves; w++) {
             std::fprintf(stderr, "  wave %d:", w);
             for (int k = 0; k < kSegs; k++) {

@@ -1741,197 +1741,6 @@ hipError_t enc_lds_t(bool verify, const EncodeArgs &a, hipStream_t s) {
     }
     return enc_lds_tt<F, LOGM, F>(verify, a, s);
 }
-// ---------------------------------------------------------------- wide-tile encode (GF(2^16), m = 64 / 256)
-// One 1024-thread workgroup per CU owns a 512-byte tile of every row: 64
-// four-symbol units (F16<1>), one per lane.  Every wave then holds the 64 units
-// of one radix-4 row quad in every pass, so every twiddle is wave-uniform: its
-// tables come in by scalar loads and feed v_perm_b32 as SGPR operands (~2.7
-// SIMD cycles per wave64 instruction against ~5 with three VGPR operands,
-// profiles/r03_valu_rate.txt), and a zero twiddle is a scalar branch.  In
-// k_enc_lds's 128-byte tiles the dist-1 and dist-4 passes have lane-varying
-// tables (vector loads, VGPR operands).  The chunk image (M rows x 512 B,
-// 128 KB at m = 256) is the only LDS state, with (lo, hi) of a unit adjacent
-// (one ds_read_b64 / ds_write_b64 per row, 512 contiguous bytes per wave);
-// the accumulator stays in VGPRs (the IFFT's last pass and the FFT's first are
-// one radix-4 group at dist M/4 with the same quad -> rows map, as in
-// k_enc_lds), and the next chunk's first-pass rows are loaded into VGPRs while
-// the current chunk runs its LDS passes.  The final FFT runs in subfield
-// coordinates (F16S).
-// leopard16.go:128-224 (encode), :685-747 (ifftDITEncoder), :618-657 (fftDIT).
-constexpr int kWideTile = 512;
-#ifndef RS_WIDE_BATCH
-#define RS_WIDE_BATCH 2  // k_enc_wide: quads a thread loads from LDS before transforming them
-#endif
-template <int LOGM, bool VERIFY>
-__global__ void __launch_bounds__(1024, 1) k_enc_wide(EncodeArgs a) {
-    typedef F16<1> F;
-    typedef F16S<1> FS;
-    typedef F::Vec V;
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    constexpr int M = 1 << LOGM, NP = LOGM / 2, D = M / 4, KQ = M / 64;  // quads per thread per pass
-    static_assert(LOGM % 2 == 0 && LOGM >= 6 && LOGM <= 8, "even log m, 64 <= m <= 256");
-    constexpr int its = ifft_slot_count(LOGM);
-    __shared__ __attribute__((aligned(16))) uint8_t lds[M * kWideTile];
-    const int lane = (int)(threadIdx.x & 63);
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t tile = (uint64_t)blockIdx.x * kWideTile;
-    const uint32_t goff = (uint32_t)((lane >> 3) * 64 + (lane & 7) * 4);  // unit `lane`'s low dword in the tile
-    const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride + tile + goff;
-    const bool uval = tile + (goff & ~63u) < a.shard_size;
-    auto lget = [&](int row) __attribute__((always_inline)) {
-        const u32x2 x = *(const __attribute__((address_space(3))) u32x2 *)(lds + row * kWideTile + lane * 8);
-        V v;
-        v.l[0] = x[0];
-        v.h[0] = x[1];
-        return v;
-    };
-    auto lput = [&](int row, const V &v) __attribute__((always_inline)) {
-        u32x2 x;
-        x[0] = v.l[0];
-        x[1] = v.h[0];
-        *(__attribute__((address_space(3))) u32x2 *)(lds + row * kWideTile + lane * 8) = x;
-    };
-    auto ld32 = [](const uint8_t *p) __attribute__((always_inline)) { return *(const __attribute__((address_space(1))) uint32_t *)p; };
-    V pf[KQ][4], acc[KQ][4];
-    auto load_chunk = [&](int c) __attribute__((always_inline)) {
-        const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
-#pragma unroll
-        for (int k = 0; k < KQ; k++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int i = 4 * (w + 16 * k) + r;
-                if (i < cnt && uval) {
-                    const uint8_t *p = row_ptr(a.data, row0 + i) + soff;
-                    pf[k][r].l[0] = ld32(p);
-                    pf[k][r].h[0] = ld32(p + 32);
-                } else {
-                    pf[k][r] = F::zero();
-                }
-            }
-    };
-    // Radix-4 pass over LDS rows at dist 4^p (IFFT) / M >> 2(p+1) (FFT); slot: first table of the pass.
-    auto lds_pass4 = [&](auto fld, auto inv, int ld, int slot, const uint32_t *tw) __attribute__((always_inline)) {
-        typedef decltype(fld) FF;
-        constexpr bool INV = decltype(inv)::value;
-        const int dist = 1 << ld;
-        constexpr int KB = KQ < RS_WIDE_BATCH ? KQ : RS_WIDE_BATCH;  // quads in flight per thread
-#pragma unroll
-        for (int k0 = 0; k0 < KQ; k0 += KB) {
-            V x[KB][4];
-#pragma unroll
-            for (int k = 0; k < KB; k++) {
-                const int q = w + 16 * (k0 + k), j = q & (dist - 1), g = q >> ld, i = g * 4 * dist + j;
-#pragma unroll
-                for (int r = 0; r < 4; r++) x[k][r] = lget(i + r * dist);
-            }
-#pragma unroll
-            for (int k = 0; k < KB; k++) {
-                const int q = w + 16 * (k0 + k), j = q & (dist - 1), g = q >> ld, i = g * 4 * dist + j;
-                const uint32_t *t = tw + (uint64_t)(slot + 3 * g) * FF::TWD;
-                if constexpr (INV) ifft4<FF>(x[k][0], x[k][1], x[k][2], x[k][3], t);
-                else fft4<FF>(x[k][0], x[k][1], x[k][2], x[k][3], t);
-#pragma unroll
-                for (int r = 0; r < 4; r++) lput(i + r * dist, x[k][r]);
-            }
-        }
-        lds_sync();
-    };
-    load_chunk(0);
-    for (int c = 0; c < a.nchunks; c++) {
-        const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
-        // pass 0 (dist 1, group = quad): from the prefetch registers
-#pragma unroll
-        for (int k = 0; k < KQ; k++) {
-            const int q = w + 16 * k;
-            ifft4<F>(pf[k][0], pf[k][1], pf[k][2], pf[k][3], tw + (uint64_t)(3 * q) * F::TWD);
-#pragma unroll
-            for (int r = 0; r < 4; r++) lput(4 * q + r, pf[k][r]);
-        }
-        if (c + 1 < a.nchunks) load_chunk(c + 1);
-        lds_sync();
-        int slot = 3 * (M / 4);
-        cfor<NP - 2>([&](auto PI) __attribute__((always_inline)) {
-            constexpr int p = decltype(PI)::value + 1;
-            lds_pass4(F{}, std::true_type{}, 2 * p, slot, tw);
-            slot += 3 * (M / (4 << (2 * p)));
-        });
-        // last pass (dist D, one group): into the accumulator
-#pragma unroll
-        for (int k = 0; k < KQ; k++) {
-            const int q = w + 16 * k;
-            V x[4];
-#pragma unroll
-            for (int r = 0; r < 4; r++) x[r] = lget(q + r * D);
-            ifft4<F>(x[0], x[1], x[2], x[3], tw + (uint64_t)slot * F::TWD);
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                if (c == 0) acc[k][r] = x[r];
-                else F::xor_into(acc[k][r], x[r]);
-            }
-        }
-        lds_sync();  // the next chunk's first pass overwrites the image
-    }
-    // fftDIT in subfield coordinates: first pass (dist D, one group) from the accumulator
-    const uint32_t *twf = a.tw_fft_sub;
-#pragma unroll
-    for (int k = 0; k < KQ; k++) {
-        const int q = w + 16 * k;
-#pragma unroll
-        for (int r = 0; r < 4; r++) sub_swap<F>(acc[k][r], a.tw_dmap);
-        fft4<FS>(acc[k][0], acc[k][1], acc[k][2], acc[k][3], twf);
-#pragma unroll
-        for (int r = 0; r < 4; r++) lput(q + r * D, acc[k][r]);
-    }
-    lds_sync();
-    int slot = 3;
-    cfor<NP - 2>([&](auto PI) __attribute__((always_inline)) {
-        constexpr int p = decltype(PI)::value + 1;
-        lds_pass4(FS{}, std::false_type{}, LOGM - 2 * (p + 1), slot, twf);
-        slot += 3 << (2 * p);
-    });
-    // last pass (dist 1, group = quad): the parity rows (or their compare)
-    uint32_t bad = 0;
-#pragma unroll
-    for (int k = 0; k < KQ; k++) {
-        const int q = w + 16 * k;
-        V x[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) x[r] = lget(4 * q + r);
-        fft4<FS>(x[0], x[1], x[2], x[3], twf + (uint64_t)(slot + 3 * q) * FS::TWD);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int row = 4 * q + r;
-            if (row < a.p && uval) {
-                sub_swap<F>(x[r], a.tw_dmap);  // back to (lo, hi)
-                uint8_t *p = row_ptr(a.parity, row) + soff;
-                if constexpr (VERIFY) {
-                    bad |= (x[r].l[0] ^ ld32(p)) | (x[r].h[0] ^ ld32(p + 32));
-                } else {
-                    *(__attribute__((address_space(1))) uint32_t *)p = x[r].l[0];
-                    *(__attribute__((address_space(1))) uint32_t *)(p + 32) = x[r].h[0];
-                }
-            }
-        }
-    }
-    if constexpr (VERIFY) flag_mismatch(a.mismatch, bad != 0);
-}
-
-// RS_ENC_WIDE=0 / 1 forces k_enc_lds / k_enc_wide for m = 64 / 256 GF(2^16)
-// encodes (parity tests cover both); unset: wide when the launch has at least
-// one workgroup per CU.
-int enc_wide_override() {
-    const char *e = getenv("RS_ENC_WIDE");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
-}
-constexpr uint64_t kWideMinGrid = 256;
-template <int LOGM>
-hipError_t enc_wide_t(bool verify, const EncodeArgs &a, hipStream_t s) {
-    const dim3 grid((unsigned)((a.shard_size + kWideTile - 1) / kWideTile), (unsigned)a.nstripes);
-    if (verify) hipLaunchKernelGGL((k_enc_wide<LOGM, true>), grid, dim3(1024), 0, s, a);
-    else hipLaunchKernelGGL((k_enc_wide<LOGM, false>), grid, dim3(1024), 0, s, a);
-    return hipGetLastError();
-}
-
 template <class F>
 hipError_t enc_lds_f(int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
     switch (logm) {
@@ -2112,12 +1921,6 @@ hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStr
 }
 
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
-    if (bits == 16 && (logm == 6 || logm == 8) && a.tw_fft_sub && a.tw_dmap) {
-        const int o = enc_wide_override();
-        const uint64_t wgs = (a.shard_size + kWideTile - 1) / kWideTile * (uint64_t)a.nstripes;
-        if (o == 1 || (o < 0 && wgs >= kWideMinGrid))
-            return logm == 8 ? enc_wide_t<8>(verify, a, s) : enc_wide_t<6>(verify, a, s);
-    }
     const bool narrow = pick_narrow((a.shard_size + 127) / 128 * (uint64_t)a.nstripes < kLdsMinGrid);
     if (narrow) return bits == 16 ? enc_lds_f<F16<2>>(logm, verify, a, s) : enc_lds_f<F8<2>>(logm, verify, a, s);
     return bits == 16 ? enc_lds_f<F16<4>>(logm, verify, a, s) : enc_lds_f<F8<4>>(logm, verify, a, s);

@@ -656,29 +656,6 @@ def test_unit_width_variants(monkeypatch, width, bits, k, p, S):
             assert np.array_equal(sh[i], full[i]), (nosub, i)
 
 
-# Wide-tile encode (k_enc_wide: 512-byte tiles, m = 64 / 256, GF(2^16)) forced
-# on and off (RS_ENC_WIDE) against the oracle: ragged chunks, k < m, p < m,
-# a partial last tile, several tiles, and verify with a tampered byte.
-@pytest.mark.parametrize("wide", ["0", "1"])
-@pytest.mark.parametrize("k,p,S", [(300, 64, 1024), (100, 40, 576), (33, 33, 512), (128, 129, 512),
-                                   (500, 200, 1088), (1024, 256, 1536), (257, 255, 64)])
-def test_wide_encode_variants(monkeypatch, wide, k, p, S):
-    monkeypatch.setenv("RS_ENC_WIDE", wide)
-    rng = np.random.default_rng(k * 3 + p + S)
-    data = rand_data(rng, k, S)
-    ref = orc.encode(16, k, p, data)
-    c = rs.ReedSolomon(k, p, 16)
-    shards = [np.ascontiguousarray(data[i]) for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
-    c.encode(shards)
-    assert np.array_equal(np.stack(shards[k:]), ref), c.encode_path
-    assert c.verify(shards)
-    shards[k + p - 1][S - 1] ^= 0x10
-    assert not c.verify(shards)
-    shards[k + p - 1][S - 1] ^= 0x10
-    shards[k // 2][S // 2] ^= 1
-    assert not c.verify(shards)
-
-
 @pytest.mark.parametrize("strided", ["data", "parity"])
 def test_device_encode_mixed_layout(torch_dev, strided):
     """One row set equally spaced (a slab), the other scattered (rows of a
