@@ -806,7 +806,7 @@ DecPlan make_plan(const RecArgs &a) {
     int u = 0;
     for (int s = 0; s < 2; s++)
         for (int e = 0; e < ne && u < G; e++) u1[8 + e][s] = u++;
-    for (int w = 7; w >= 0 && u < G; w--) u1[w][0] = u++;
+    for (int w = 7; w >= 0 && u < G; w--) u1[w][0] = u++;  // which waves: no measurable difference (profiles/r03_c4_plan_ab.txt)
     if (u < G) {  // more units than the plan can hold: the launcher falls back
         DecPlan bad{};
         bad.ntiles = -1;
