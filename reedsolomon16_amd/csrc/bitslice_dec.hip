@@ -707,17 +707,32 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
 #endif
     for (;;) {
         const bool cur = t >= 0, more = tn < pl.ntiles;
-        const bool early_p1 = early && more && u1a >= 0;  // passes phase 2's barriers inside its first unit
+        // The first iteration has no phase 2 / 3: every wave is free, so
+        // wave w takes phase-1 unit w (one each) instead of the plan's split.
+        const bool first = t < 0;
+        const int p1a = first ? (w < kUnits ? w : -1) : u1a, p1b = first ? -1 : u1b;
+        const bool early_p1 = early && more && p1a >= 0;  // passes phase 2's barriers inside its first unit
+        // The last iteration has no phase 1: waves 8.. take the second phase-3
+        // units of waves 0.. (so every phase-3 unit runs on a wave of its own).
+        int p3a = u3a, p3b = u3b;
+        if (!more) {
+            if (early) {
+                p3a = (int)((uint32_t)(pl.code[0] >> (16 * (w - 8))) >> 4 & 15u) - 1;
+                p3b = -1;
+            } else if (w + 8 < kWaves) {
+                p3b = -1;
+            }
+        }
         if (early_p1) {
             // ---- early phase 1 of tile tn (registers only); a first unit parks in V[8..15]
             set_tile(tn);
-            const int n1 = u1b >= 0 ? 2 : 1;
+            const int n1 = p1b >= 0 ? 2 : 1;
             // (loading unit b's rows into V[8..15] up front measured slower:
             // 1950 vs 1694 us per 16 C4 stripes)
 #pragma nounroll
             for (int s = 0; s < n1; s++) {  // one copy of the phase-1 code
                 if (s) d.park_swap();
-                d.phase1(s ? u1b : u1a, false, s == 0 && cur ? 2 : 0);
+                d.phase1(s ? p1b : p1a, false, s == 0 && cur ? 2 : 0);
             }
         }
         STAMP(12);
@@ -736,35 +751,35 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
             }
             if (!early_p1) lds_barrier();  // Y is in the image
             STAMP(2);
-            if (u3a >= 0) {
+            if (p3a >= 0) {
                 // ---- phase 3 of tile t, one unit at a time (each read from the
                 // image before the barrier below frees it)
                 set_tile(t);
-                const int n3 = u3b >= 0 ? 2 : 1;
+                const int n3 = p3b >= 0 ? 2 : 1;
 #pragma nounroll
                 for (int s = 0; s < n3; s++) {
-                    const int u = s ? u3b : u3a;
+                    const int u = s ? p3b : p3a;
                     d.template unit_get<0>(u);
                     d.phase3(u);
                 }
             }
             STAMP(4);
         }
-        if (!early && more && u1a >= 0) {
+        if (!early && more && p1a >= 0) {
             // ---- late phase 1 of tile tn (registers only)
             set_tile(tn);
-            d.phase1(u1a, false);
+            d.phase1(p1a, false);
         }
         STAMP(5);
         if (!more) break;
         lds_barrier();  // the image is free for phase 1 of tile tn
         STAMP(3);
-        if (u1a >= 0) {
+        if (p1a >= 0) {
             if (early) {
-                d.template unit_put<0>(u1b >= 0 ? u1b : u1a);
-                if (u1b >= 0) d.template unit_put<8>(u1a);
+                d.template unit_put<0>(p1b >= 0 ? p1b : p1a);
+                if (p1b >= 0) d.template unit_put<8>(p1a);
             } else {
-                d.template unit_put<0>(u1a);
+                d.template unit_put<0>(p1a);
             }
         }
         lds_barrier();  // u of tile tn is in the image
