@@ -191,3 +191,23 @@ def test_simd_port_matches_scalar_oracle(k, p, S, threads, isa):
     rng = np.random.default_rng(k + p + S + threads)
     data = rng.integers(0, 256, (k, S), dtype=np.uint8)
     assert np.array_equal(orc.encode_simd(k, p, data, threads, isa=isa), orc.encode(16, k, p, data))
+
+
+def test_c5_chunk_twiddles_are_chunk0_plus_layer_constant():
+    """The structure behind a bit-sliced m = 256 encode:
+    FFTInitialize builds fftSkew[j + 2^(i+1)] = fftSkew[j] ^ temp[i]
+    (leopard16.go:877-900), so the twiddles of chunk c's ifftDITEncoder
+    (skew offset (c+1)*m - 1, leopard16.go:153-171) are chunk 0's XOR a
+    constant per layer: 8 distinct differences per chunk at m = 256, i.e.
+    one full-field constant network per (layer, chunk) on top of networks
+    shared by every chunk."""
+    log, exp, skew, _ = orc.tables16()
+    raw = np.where(skew == 65535, 0, exp[np.minimum(skew, 65534)].astype(np.int64))
+    m = 256
+    j = np.arange(1, m)
+    for c in range(1, 4):
+        d = raw[(c + 1) * m - 1 + j] ^ raw[m - 1 + j]
+        layer = np.floor(np.log2(j & -j)).astype(int)  # lowest set bit of j: the butterfly layer of slot j
+        for L in range(8):
+            assert len(set(d[layer == L].tolist())) == 1, (c, L)
+        assert len(set(d.tolist())) == 8
