@@ -55,6 +55,7 @@
 #include <map>
 #include <mutex>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "bs_common.hpp"
@@ -809,38 +810,64 @@ DecPlan make_plan(const RecArgs &a) {
         if ((a.need[u >> 1] >> (16 * (u & 1))) & 0xFFFFu) rmask |= 1u << u;
     static std::mutex mu;
     static std::map<uint32_t, DecPlan> cache;
-    const uint32_t key = (uint32_t)G << 16 | rmask;
+    const uint32_t key = (uint32_t)a.mtrunc << 16 | rmask;  // the costs depend on which units lie past mtrunc
     {
         std::lock_guard<std::mutex> lk(mu);
         auto it = cache.find(key);
         if (it != cache.end()) return it->second;
     }
-    int u1[kWaves][2], u3[kWaves][2];
-    for (int w = 0; w < kWaves; w++) u1[w][0] = u1[w][1] = u3[w][0] = u3[w][1] = -1;
+    // Cost model (cycles per tile, from RS_DEC_STAMP runs at C4): a phase-1
+    // unit 27 k (a unit past mtrunc only writes zeros: 1 k), a phase-3 unit
+    // 14 k, phase 2 plus the exchange 17 k before a wave < 8 starts its units;
+    // the early waves start at once.  E phase-1 units go to the early waves
+    // (at most two each), the rest one per wave < 8 from wave 7 down, and the
+    // phase-3 units one by one to the cheapest wave < 8 (at most two each);
+    // the E with the smallest maximum wins (ties: the larger E).  C4 with 32
+    // erasures (ten phase-3 units) gets E = 8; few-erasure repairs get E = 4,
+    // spreading phase 1 over the waves phase 3 leaves idle.
     const int ne = kWaves - 8;
-    int u = 0;
-    for (int s = 0; s < 2; s++)
-        for (int e = 0; e < ne && u < G; e++) u1[8 + e][s] = u++;
-    for (int w = 7; w >= 0 && u < G; w--) u1[w][0] = u++;  // which waves: no measurable difference (profiles/r03_c4_plan_ab.txt)
-    if (u < G) {  // more units than the plan can hold: the launcher falls back
+    auto c1 = [&](int uu) { return 16 * uu < a.mtrunc ? 27 : 1; };
+    int u1[kWaves][2], u3[kWaves][2];
+    int best = INT_MAX;
+    for (int E = std::min(G, 2 * ne); E >= 0; E--) {
+        if (G - E > 8) break;
+        int t1[kWaves][2], t3[kWaves][2], cost[kWaves] = {0};
+        for (int w = 0; w < kWaves; w++) t1[w][0] = t1[w][1] = t3[w][0] = t3[w][1] = -1;
+        for (int i = 0; i < E; i++) {
+            t1[8 + i % ne][i / ne] = i;
+            cost[8 + i % ne] += c1(i);
+        }
+        for (int w = 0; w < 8; w++) cost[w] = 17;
+        for (int i = E, w = 7; i < G; i++, w--) {
+            t1[w][0] = i;
+            cost[w] += c1(i);
+        }
+        bool ok = true;
+        for (int g = 0; g < G && ok; g++) {
+            if (!((rmask >> g) & 1)) continue;
+            int bw = -1;
+            for (int w = 0; w < 8; w++)
+                if (t3[w][1] < 0 && (bw < 0 || cost[w] < cost[bw])) bw = w;
+            if (bw < 0) {
+                ok = false;
+                break;
+            }
+            t3[bw][t3[bw][0] < 0 ? 0 : 1] = g;
+            cost[bw] += 14;
+        }
+        if (!ok) continue;
+        int mx = 0;
+        for (int w = 0; w < kWaves; w++) mx = std::max(mx, cost[w]);
+        if (mx < best) {
+            best = mx;
+            std::memcpy(u1, t1, sizeof u1);
+            std::memcpy(u3, t3, sizeof u3);
+        }
+    }
+    if (best == INT_MAX) {  // cannot happen for G <= 10 units
         DecPlan bad{};
         bad.ntiles = -1;
         return bad;
-    }
-    int free3[8], nf = 0;
-    for (int w = 0; w < 8; w++)
-        if (u1[w][0] < 0) free3[nf++] = w;
-    int j = 0;
-    for (int g = 0; g < G; g++) {
-        if (!((rmask >> g) & 1)) continue;
-        const int w = free3[j % nf], s = j / nf;
-        if (s > 1) {
-            DecPlan bad{};
-            bad.ntiles = -1;
-            return bad;
-        }
-        u3[w][s] = g;
-        j++;
     }
     DecPlan bp{};
     for (int w = 0; w < kWaves; w++) {
