@@ -31,7 +31,9 @@ around the timed launches, divided by their count).  `single_stripe` repeats
 the kernel timing with one stripe per launch (the reference's Encode
 granularity).  Resident rows sit at a stride of row bytes + --row-pad (3 KiB
 by default); `unpadded_rows` times the same launch on rows
-packed exactly one row length apart.  `cpu_baseline` times the reference-equivalent AVX2 and AVX-512 ports of the
+packed exactly one row length apart.  `other_workloads` (one GPU) reports the
+kernel time and roofline fraction of the C4 reconstruct and the C5 encode
+beside the headline.  `cpu_baseline` times the reference-equivalent AVX2 and AVX-512 ports of the
 encode (oracle/leopard_ref.c, test/bench infrastructure) on a bounded sample:
 1 thread (the reference is single-threaded per call) and N threads over byte
 ranges.
@@ -124,6 +126,55 @@ def load_traffic(kernel_name: str, workload: str, stripes: int):
         return None
 
 
+def other_workloads(torch, rs, dev, stream) -> dict:
+    """Kernel time of the other BASELINE configs on this GPU, beside the
+    headline (reported, not the metric): C4 = reconstruct of 128+32 x 1 MiB
+    with 32 erased shards, 16 stripes per launch (rs_reconstruct_dev_batch);
+    C5 = encode of 1024+256 x 256 KiB, 32 stripes per launch.  Algorithmic
+    bytes: rows read + rows written per stripe (C4: 128 + 32, C5: 1024 + 256)."""
+    import numpy as np
+
+    out = {}
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xC4C5)
+
+    def kernel_ms(fn, n):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(n):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n
+
+    k, p, S, ns = 128, 32, 1 << 20, 16
+    c4 = rs.New16(k, p, device=dev.index)
+    slab = torch.randint(0, 256, (ns, k + p, S), dtype=torch.uint8, device=dev, generator=g)
+    c4.encode_dev_batch(slab, stream)
+    present = np.ones(k + p, bool)
+    present[np.random.default_rng(0x5EED).choice(k + p, p, replace=False)] = False
+    ms = kernel_ms(lambda: c4.reconstruct_dev_batch(slab, present, stream=stream), 20)
+    alg = ns * (k + p) * S
+    out["C4_reconstruct"] = {"config": "128+32 x 1024 KiB, 32 erased shards, 16 stripes per launch",
+                             "kernel_ms": round(ms, 5), "us_per_stripe": round(ms * 1e3 / ns, 2),
+                             "alg_bytes_per_launch": alg, "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    del slab
+    k, p, S, ns = 1024, 256, 256 << 10, 32
+    c5 = rs.New16(k, p, device=dev.index)
+    slab = torch.randint(0, 256, (ns, k + p, S), dtype=torch.uint8, device=dev, generator=g)
+    ms = kernel_ms(lambda: c5.encode_dev_batch(slab, stream), 10)
+    alg = ns * (k + p) * S
+    out["C5_encode"] = {"config": "1024+256 x 256 KiB, 32 stripes per launch", "kernel_path": c5.encode_path,
+                        "kernel_ms": round(ms, 5), "us_per_stripe": round(ms * 1e3 / ns, 2),
+                        "alg_bytes_per_launch": alg, "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    del slab
+    torch.cuda.empty_cache()
+    return out
+
+
 def free_port() -> int:
     import socket
 
@@ -183,6 +234,7 @@ def main():
                          "64-byte multiple); the unpadded layout is timed too and reported beside it")
     ap.add_argument("--no-unpadded", action="store_true", help="skip timing the unpadded layout")
     ap.add_argument("--dry-run", action="store_true", help="rank layout only: gloo on the CPU, no GPU")
+    ap.add_argument("--no-other", action="store_true", help="skip the C4 / C5 kernel figures (one GPU only)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -276,6 +328,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el, kern_ms, one_ms, flat_ms = float(t[0]), float(t[1]), float(t[2]) or None, float(t[3]) or None
 
+    other = None
+    if world == 1 and not args.no_other:
+        del buf, slab, flat
+        torch.cuda.empty_cache()
+        other = other_workloads(torch, rs, dev, stream)
+
     ms_per_step = el / args.steps * 1e3
     job_stripes = B if args.split == "bytes" else world * B
     data_bytes = args.steps * job_stripes * K * S
@@ -334,6 +392,7 @@ def main():
                 "frac": round((K + P) * W / (one_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
             },
             "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(K, P, S, args.cpu_seconds, threads),
+            "other_workloads": other,
         }
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -16,10 +16,10 @@ timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke(); print("smok
 rc=$?; echo "smoke rc=$rc"; tail -2 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py $BARGS > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu --no-single --no-unpadded $BARGS > $OUT/trace_bench.json 2> $OUT/trace.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu --no-single --no-unpadded --no-other $BARGS > $OUT/trace_bench.json 2> $OUT/trace.err
 rc=$?; echo "trace rc=$rc"; cat $OUT/trace_bench.json; [ $rc -eq 0 ] || exit $rc
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o run -- python3 bench.py --no-cpu --no-single --no-unpadded --steps 50 --warmup 5 > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o run -- python3 bench.py --no-cpu --no-single --no-unpadded --no-other --steps 50 --warmup 5 > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 exit 0
