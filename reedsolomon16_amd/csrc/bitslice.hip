@@ -213,6 +213,11 @@ struct HpEncoder {
         uint32_t voff = (uint32_t)L.ct * TILE + (uint32_t)blk * 64 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
         constexpr uint32_t QS = 16;
         asm volatile("" : "+v"(voff));
+        // the loads issue at raised wave priority, ahead of the other waves'
+        // VALU: one stripe per launch 0.524-0.527 -> 0.547-0.552 of the
+        // roofline, 128 stripes unchanged (same box, profiles/r03_c3_prio_ab.txt;
+        // raising it around the parity stores too gained nothing)
+        __builtin_amdgcn_s_setprio(2);
 #pragma unroll
         for (int i = I0; i < I1; i++) {
             // wave-uniform row of the h = 0 lanes (rows >= k are out of range: zeros)
@@ -224,6 +229,7 @@ struct HpEncoder {
                 d[0] = x[0], d[1] = x[1], d[2] = x[2], d[3] = x[3];
             }
         }
+        __builtin_amdgcn_s_setprio(0);
     }
 
     // IFFT layers r0 .. r(LR-1) on rows RW*W + j.

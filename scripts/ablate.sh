@@ -17,5 +17,5 @@ done
 wait
 for d in build/ablate/*/; do
   [ "$(basename $d)" = common ] && continue
-  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $d/librs_mi355x.so $d/kernels.o reedsolomon16_amd/build/bitslice.o build/ablate/common/gf_host.o build/ablate/common/codec.o
+  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $d/librs_mi355x.so $d/kernels.o reedsolomon16_amd/build/bitslice.o reedsolomon16_amd/build/bitslice_dec.o build/ablate/common/gf_host.o build/ablate/common/codec.o
 done

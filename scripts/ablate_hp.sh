@@ -18,5 +18,5 @@ done
 wait
 for d in $OUT/*/; do
   [ "$(basename $d)" = common ] && continue
-  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $d/librs_mi355x.so $B/kernels.o $d/bitslice.o $B/gf_host.o $B/codec.o
+  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $d/librs_mi355x.so $B/kernels.o $d/bitslice.o $B/bitslice_dec.o $B/gf_host.o $B/codec.o
 done
