@@ -726,6 +726,11 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
         }
         if (early_p1) {
             // ---- early phase 1 of tile tn (registers only); a first unit parks in V[8..15]
+            // The early waves' chain is the critical path: it issues ahead of
+            // the phase-2 / phase-3 waves sharing its SIMD (C4 x 16 1692 ->
+            // 1637 us, one stripe 124 -> 121 us; raising the phase-3 waves too
+            // gained nothing, profiles/r03_c4_prio_ab.txt).
+            __builtin_amdgcn_s_setprio(3);
             set_tile(tn);
             const int n1 = p1b >= 0 ? 2 : 1;
             // (loading unit b's rows into V[8..15] up front measured slower:
@@ -735,6 +740,7 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
                 if (s) d.park_swap();
                 d.phase1(s ? p1b : p1a, false, s == 0 && cur ? 2 : 0);
             }
+            __builtin_amdgcn_s_setprio(0);
         }
         STAMP(12);
         if (cur) {
