@@ -204,11 +204,6 @@ typedef __attribute__((address_space(4))) const RecArgs cargs_t;
     } while (0)
 #endif
 [[maybe_unused]] constexpr int kSegs = 16;
-// Where an early wave passes phase 2's barriers inside its first phase-1
-// unit: 1 after the scaling, 2 after IFFT layer 0, 3 after the transpose.
-#ifndef RS_DEC_EARLY_BAR
-#define RS_DEC_EARLY_BAR 2
-#endif
 
 template <bool STRIDED>
 struct Dec {
@@ -440,11 +435,12 @@ struct Dec {
             });
         });
     }
-    // the phase-1 transform of unit u, from its rows in HBM (loads already
-    // issued when `loaded`) to planes in V[0..7]
-    // nbar: workgroup barriers to pass after the scaling (an early wave passes
-    // phase 2's two barriers there, so it does not hold phase 2 back)
-    __device__ __forceinline__ void phase1(int u, bool loaded, int nbar = 0) {
+    // the phase-1 transform of unit u, from its rows in HBM to planes in V[0..7].
+    // nbar: workgroup barriers to pass after IFFT layer 0 (an early wave passes
+    // phase 2's two barriers there, so it does not hold phase 2 back; after the
+    // scaling / after the transpose measured 1753 / 1704 against 1690 us per
+    // 16 C4 stripes, profiles/r03_c4_bsdec_units_ab.txt)
+    __device__ __forceinline__ void phase1(int u, int nbar = 0) {
         if (16 * u >= args().mtrunc) {  // rows past mtrunc: zero (the image rows still have to be written)
 #pragma unroll
             for (int i = 0; i < 8; i++)
@@ -453,17 +449,11 @@ struct Dec {
             for (int b = 0; b < nbar; b++) lds_barrier();
             return;
         }
-        if (!loaded)
-            if constexpr (!ABL(0)) load_rows(u);
+        if constexpr (!ABL(0)) load_rows(u);
         scale(u);
-        if (RS_DEC_EARLY_BAR == 1)
-            for (int b = 0; b < nbar; b++) lds_barrier();
         if constexpr (!ABL(1)) ifft0_bytes(u);
-        if (RS_DEC_EARLY_BAR == 2)
-            for (int b = 0; b < nbar; b++) lds_barrier();
+        for (int b = 0; b < nbar; b++) lds_barrier();
         to_planes(0xFFu);
-        if (RS_DEC_EARLY_BAR == 3)
-            for (int b = 0; b < nbar; b++) lds_barrier();
         if constexpr (!ABL(1)) ifft_a(u);
     }
     // V[0..7] <-> V[8..15] (the parked unit)
@@ -738,7 +728,7 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
 #pragma nounroll
             for (int s = 0; s < n1; s++) {  // one copy of the phase-1 code
                 if (s) d.park_swap();
-                d.phase1(s ? p1b : p1a, false, s == 0 && cur ? 2 : 0);
+                d.phase1(s ? p1b : p1a, s == 0 && cur ? 2 : 0);
             }
             __builtin_amdgcn_s_setprio(0);
         }
@@ -775,7 +765,7 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
         if (!early && more && p1a >= 0) {
             // ---- late phase 1 of tile tn (registers only)
             set_tile(tn);
-            d.phase1(p1a, false);
+            d.phase1(p1a);
         }
         STAMP(5);
         if (!more) break;
