@@ -229,6 +229,12 @@ int rs_debug_split_check(int logm, uint32_t seed);
  * byte-permute multiply and half-wave layout): data = k rows of S bytes,
  * parity = p rows of S bytes.  GF(2^16) codecs with 4 <= m <= 32 only. */
 int rs_debug_split_emulate(rs_codec *codec, const uint8_t *data, uint8_t *parity, size_t shard_size);
+/* The bit-sliced n = 256 reconstruct's wave plan (csrc/bitslice_dec.hip
+ * make_plan) for work rows [0, mtrunc) with revealed-row mask need[8] (bit r:
+ * work row r): per wave w, bits 16 (w % 4) .. of code[w / 4] hold four 4-bit
+ * fields (unit + 1, 0 = none): phase-3 units 0, 1, phase-1 units 0, 1.
+ * Returns 0, or -1 when the kernel does not serve mtrunc.  Host only. */
+int rs_debug_dec_plan(int mtrunc, const uint32_t *need, uint64_t *code);
 
 /* Human-readable message for an error code. */
 const char *rs_strerror(int code);

@@ -71,6 +71,7 @@ def lib() -> C.CDLL:
     L.rs_debug_sub_twiddle.argtypes = [C.c_uint32, vp]
     L.rs_debug_sub_swap.argtypes = [C.c_uint32]
     L.rs_debug_sub_swap.restype = C.c_uint32
+    L.rs_debug_dec_plan.argtypes = [i32, vp, vp]
     _lib = L
     return L
 

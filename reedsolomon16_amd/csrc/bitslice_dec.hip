@@ -878,6 +878,17 @@ DecPlan make_plan(const RecArgs &a) {
 
 }  // namespace
 
+extern "C" int rs_debug_dec_plan(int mtrunc, const uint32_t *need, uint64_t *code) {
+    if (mtrunc < 1 || mtrunc > kImgRows || !need || !code) return -1;
+    RecArgs a{};
+    a.mtrunc = mtrunc;
+    for (int k = 0; k < 8; k++) a.need[k] = need[k];
+    const DecPlan pl = make_plan(a);
+    if (pl.ntiles < 0) return -1;
+    for (int j = 0; j < 3; j++) code[j] = pl.code[j];
+    return 0;
+}
+
 bool rec_bs256_available(int bits, int logn, bool sub, int mtrunc) {
     return bits == 16 && logn == 8 && sub && mtrunc <= kImgRows;
 }

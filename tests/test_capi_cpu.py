@@ -289,3 +289,53 @@ def test_split_c_abi_matches_go_model(k, p, n):
     buf = io.BytesIO()
     c.join(buf, got, n)
     assert buf.getvalue() == data.tobytes()
+
+
+def _dec_plan(mtrunc, need):
+    import ctypes as C
+
+    L = rs._capi.lib()
+    nd = (C.c_uint32 * 8)(*need)
+    code = (C.c_uint64 * 3)()
+    assert L.rs_debug_dec_plan(mtrunc, nd, code) == 0
+    waves = []
+    for w in range(12):
+        c = (code[w // 4] >> (16 * (w % 4))) & 0xFFFF
+        waves.append([((c >> (4 * f)) & 15) - 1 for f in range(4)])  # u3a, u3b, u1a, u1b
+    return waves
+
+
+@pytest.mark.parametrize("mtrunc", [160, 152, 129, 100, 33])
+def test_bsdec_plan_covers_every_unit(mtrunc):
+    """The bit-sliced decoder's host plan (bitslice_dec.hip make_plan): every
+    16-row unit gets exactly one phase-1 slot, the units with a revealed row
+    exactly one phase-3 slot, waves >= 8 (which run phase 1 during phase 2)
+    hold no phase-3 unit, waves < 8 at most one phase-1 unit (the kernel's late
+    path runs only the first), and the last iteration's remap (waves 8..11 take
+    the second phase-3 unit of waves 0..3) still covers every phase-3 unit."""
+    rng = np.random.default_rng(mtrunc)
+    cases = [0, (1 << 10) - 1, 1, 1 << 9, 0b1010101010] + [int(x) for x in rng.integers(0, 1 << 10, 60)]
+    units = (mtrunc + 15) // 16
+    for mask in cases:
+        need = [0] * 8
+        rev = set()
+        for u in range(units):
+            if (mask >> u) & 1:
+                r = min(16 * u + int(rng.integers(0, 16)), mtrunc - 1)
+                need[r >> 5] |= 1 << (r & 31)
+                rev.add(r // 16)
+        waves = _dec_plan(mtrunc, need)
+        p1 = sorted(u for w in waves for u in w[2:] if u >= 0)
+        assert p1 == list(range(10)), (mask, waves)
+        p3 = sorted(u for w in waves for u in w[:2] if u >= 0)
+        assert p3 == sorted(rev), (mask, waves)
+        for w, (u3a, u3b, u1a, u1b) in enumerate(waves):
+            assert u3b < 0 or u3a >= 0
+            assert u1b < 0 or u1a >= 0
+            if w >= 8:
+                assert u3a < 0 and u3b < 0
+            else:
+                assert u1b < 0
+        last = [u for w in range(8) for u in (waves[w][:1] if w < 4 else waves[w][:2]) if u >= 0]
+        last += [waves[w - 8][1] for w in range(8, 12) if waves[w - 8][1] >= 0]
+        assert sorted(last) == sorted(rev)
