@@ -95,7 +95,8 @@ int rs_verify(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int n
  * rs_encode_query are the same functions).  Same validation and errors as the
  * synchronous calls.  rs_reconstruct_async sets lens[i] = S for the shards it
  * will rebuild at call time; when nothing is missing it returns RS_OK with
- * *ticket = 0 (no work queued).  Rebuilt rows in pageable memory make the call
+ * *ticket = 0 (no work queued), which rs_ticket_wait / rs_ticket_query report
+ * as complete.  Rebuilt rows in pageable memory make the call
  * synchronous (bounce slab), as for encode. */
 int rs_verify_async(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nshards, uint64_t *ticket);
 /* Waits for a verify ticket and reports *ok = 1 iff its parity matched.

@@ -292,7 +292,9 @@ class ReedSolomon:
     def reconstruct_async(self, shards: list, recover_all: bool = True) -> "EncodeTicket":
         """Queue a Reconstruct (rs_reconstruct_async).  Missing entries of
         `shards` are replaced at call time by the buffers the rebuilt shards
-        will land in; their bytes are final once the ticket's wait() returns."""
+        will land in (the EmptyShard's own row, else a fresh pinned row); their
+        bytes are final once the ticket's wait() returns.  A stripe with nothing
+        to rebuild gets ticket 0, which is done at once."""
         keep = []
         t = self._reconstruct(shards, recover_all, ticket=True, keep=keep)
         return EncodeTicket(self, t, keep)
@@ -309,7 +311,9 @@ class ReedSolomon:
                 # make([]byte, shardSize) (leopard16.go:556-560); fully overwritten
                 bufs[i] = _capacity_view(bufs[i], S)
                 if bufs[i] is None:
-                    bufs[i] = np.empty(S, dtype=np.uint8)
+                    # a ticket's rebuilt rows go into pinned memory: pageable
+                    # outputs would make the queued call synchronous (bounce slab)
+                    bufs[i] = alloc_pinned(S) if ticket else np.empty(S, dtype=np.uint8)
         ptrs = (C.c_void_p * total)()
         lens = (C.c_size_t * total)()
         for i, s in enumerate(shards):
@@ -512,12 +516,15 @@ class EncodeTicket:
         self.codec, self.ticket, self._keep = codec, ticket, keep
 
     def done(self) -> bool:
+        if self.ticket == 0:
+            return True
         d = C.c_int(0)
         _check(self.codec._L.rs_ticket_query(self.codec._h, self.ticket, C.byref(d)))
         return bool(d.value)
 
     def wait(self) -> None:
-        _check(self.codec._L.rs_ticket_wait(self.codec._h, self.ticket))
+        if self.ticket:
+            _check(self.codec._L.rs_ticket_wait(self.codec._h, self.ticket))
         self._keep = None
 
 

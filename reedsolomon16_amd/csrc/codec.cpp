@@ -101,6 +101,17 @@ struct DevPlan {
     hipError_t mark_used(hipStream_t s) {
         for (auto &u : used)
             if (u.first == s) return hipEventRecord(u.second, s);
+        // a new stream: first drop the streams whose last launch has finished
+        // (short-lived caller streams would otherwise pile up events)
+        for (size_t i = 0; i < used.size();) {
+            if (hipEventQuery(used[i].second) == hipSuccess) {
+                (void)hipEventDestroy(used[i].second);
+                used[i] = used.back();
+                used.pop_back();
+            } else {
+                i++;
+            }
+        }
         hipEvent_t ev = nullptr;
         hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
         if (e != hipSuccess) return e;
@@ -1107,8 +1118,9 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     // reads; it waits only on ev_free[b].
     const uint64_t stage_cap = (uint64_t)c->stage.n / kHostBufs;  // >= slab_al
     // scratch of the multi-pass paths, sized before any launch (no realloc mid-pipeline)
-    if (op == HostOp::Reconstruct) e = scratch_ensure(c, c->work, (size_t)c->n * seg);
-    else if (c->logm > kMaxRegLogM) e = scratch_ensure(c, c->work, (size_t)2 * c->m * seg);
+    // (the n <= 256 reconstruct plan and the m <= 256 LDS encode use none)
+    if (op == HostOp::Reconstruct && !dpl) e = scratch_ensure(c, c->work, (size_t)c->n * seg);
+    else if (op != HostOp::Reconstruct && c->logm > kMaxLdsLogN) e = scratch_ensure(c, c->work, (size_t)2 * c->m * seg);
     if (e) return e;
     // outputs in pageable memory go D2H into a pinned bounce slab, and the host
     // copies segment j - 1 out while the device works on segment j
@@ -1621,7 +1633,11 @@ int rs_encode_query(rs_codec *c, uint64_t ticket, int *done) {
     hipEvent_t ev;
     {
         std::lock_guard<std::mutex> lk(c->mu);
-        if (ticket == 0 || ticket >= c->next_ticket) return RS_ERR_INVALID_ARG;
+        if (ticket >= c->next_ticket) return RS_ERR_INVALID_ARG;
+        if (ticket == 0) {  // no work was queued (rs_reconstruct_async with nothing missing)
+            *done = 1;
+            return RS_OK;
+        }
         ev = c->done_ev[ticket % rs_codec::kTickets];
     }
     DeviceGuard g(c->device);
@@ -1640,7 +1656,8 @@ int rs_encode_wait(rs_codec *c, uint64_t ticket) {
     hipEvent_t ev;
     {
         std::lock_guard<std::mutex> lk(c->mu);
-        if (ticket == 0 || ticket >= c->next_ticket) return RS_ERR_INVALID_ARG;
+        if (ticket >= c->next_ticket) return RS_ERR_INVALID_ARG;
+        if (ticket == 0) return RS_OK;  // no work was queued
         // an event slot reused by a later call completes after this ticket's
         // work (same streams, queue order): waiting on it is still correct
         ev = c->done_ev[ticket % rs_codec::kTickets];
@@ -1672,18 +1689,22 @@ int rs_verify_async(rs_codec *c, uint8_t *const *shards, const size_t *lens, int
 int rs_verify_result(rs_codec *c, uint64_t ticket, int *ok) {
     if (!c || !ok) return RS_ERR_INVALID_ARG;
     *ok = 0;
-    int *h;
+    const int slot = (int)(ticket % rs_codec::kTickets);
+    // the slot must still hold this verify ticket (not reused by a later call)
+    auto owns_slot = [&] {
+        return ticket != 0 && ticket < c->next_ticket && ticket + rs_codec::kTickets >= c->next_ticket &&
+               c->tk_kind[slot] == (uint8_t)((int)HostOp::Verify + 1) && c->tk_hflag;
+    };
     {
         std::lock_guard<std::mutex> lk(c->mu);
-        const int slot = (int)(ticket % rs_codec::kTickets);
-        // the slot must still hold this verify ticket (not reused by a later call)
-        if (ticket == 0 || ticket >= c->next_ticket || ticket + rs_codec::kTickets < c->next_ticket ||
-            c->tk_kind[slot] != (uint8_t)((int)HostOp::Verify + 1) || !c->tk_hflag)
-            return RS_ERR_INVALID_ARG;
-        h = c->tk_hflag + slot;
+        if (!owns_slot()) return RS_ERR_INVALID_ARG;
     }
     if (int e = rs_encode_wait(c, ticket)) return e;
-    *ok = *(volatile int *)h == 0;
+    // read the verdict under the lock, after checking again that no later call
+    // (ticket + kTickets) has taken the slot and rewritten its flag meanwhile
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!owns_slot()) return RS_ERR_INVALID_ARG;
+    *ok = *(volatile int *)(c->tk_hflag + slot) == 0;
     return RS_OK;
 }
 
@@ -1708,7 +1729,7 @@ int rs_verify(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshar
 
 namespace {
 // rs_reconstruct / rs_reconstruct_async.  Nothing to rebuild: RS_OK with no
-// ticket issued (*ticket stays 0; waiting on ticket 0 is RS_ERR_INVALID_ARG).
+// ticket issued (*ticket stays 0, which rs_ticket_wait / query report as done).
 int reconstruct_host(rs_codec *c, uint8_t *const *shards, size_t *lens, int nshards, int recover_all, uint64_t *ticket) {
     if (!c || !shards || !lens) return RS_ERR_INVALID_ARG;
     if (nshards != c->total) return RS_ERR_TOO_FEW_SHARDS;
