@@ -110,20 +110,28 @@ def cpu_baseline(K, P, S, seconds: float, threads: int):
                        + "; ".join(notes))}
 
 
-def load_traffic(kernel_name: str, workload: str, stripes: int):
+def traffic_key(workload: str, kernel_name: str, stripes: int, row_bytes: int) -> str:
+    """profiles/pmc_traffic.json key: the launch shape one rank runs (its
+    stripes per launch and bytes of every row, i.e. its byte-range slice)."""
+    return f"{workload}:{kernel_name}:{stripes}x{row_bytes}"
+
+
+def load_traffic(kernel_name: str, workload: str, stripes: int, row_bytes: int, shard_bytes: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, scripts/collect_profiles.py), if it was taken
-    for this workload and batch size."""
+    for this workload, batch size and per-rank row slice."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        e = d.get(f"{workload}:{kernel_name}") or (d.get(kernel_name) if workload == "C3" else None)
-        if not e or e.get("stripes", 16) != stripes:
-            return None
-        return e.get("hbm_bytes_per_launch")
     except Exception:
         return None
+    e = d.get(traffic_key(workload, kernel_name, stripes, row_bytes))
+    if e is None and row_bytes == shard_bytes:  # entries written before the per-slice keys
+        e = d.get(f"{workload}:{kernel_name}") or (d.get(kernel_name) if workload == "C3" else None)
+        if e and e.get("stripes", 16) != stripes:
+            e = None
+    return e.get("hbm_bytes_per_launch") if e else None
 
 
 def other_workloads(torch, rs, dev, stream) -> dict:
@@ -208,11 +216,22 @@ def dry_run(args, rank: int, world: int) -> None:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
     K, P, S = WORKLOADS[args.workload]
     lo, hi = rsd.byte_range(S, rank, world) if args.split == "bytes" else (0, S)
+    kname = "bs16-m32" if args.workload == "C3" else "lds-m256"  # the engine's path for the workload (rs_encode_path)
     got = [None] * world
-    dist.all_gather_object(got, {"rank": rank, "byte_range": [lo, hi], "world": dist.get_world_size()})
+    dist.all_gather_object(got, {"rank": rank, "byte_range": [lo, hi], "world": dist.get_world_size(),
+                                 "traffic_key": traffic_key(args.workload, kname, args.stripes, hi - lo),
+                                 "traffic": load_traffic(kname, args.workload, args.stripes, hi - lo, S)})
     if rank == 0:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_requested": args.gpus, "workload": args.workload,
-                          "split": args.split, "ranks": got}), flush=True)
+                          "split": args.split, "ranks": got,
+                          # the evidence keys of a real N-rank line (kernel times need a GPU)
+                          "roofline": {"traffic": got[0]["traffic"], "traffic_key": got[0]["traffic_key"],
+                                       "per_rank_traffic": [r["traffic"] for r in got]},
+                          "per_rank_frac": [None] * world,
+                          "cpu_baseline": None if args.no_cpu else cpu_baseline(K, P, S, args.cpu_seconds, threads)}),
+              flush=True)
+    dist.barrier()
     dist.destroy_process_group()
 
 
@@ -235,6 +254,9 @@ def main():
     ap.add_argument("--no-unpadded", action="store_true", help="skip timing the unpadded layout")
     ap.add_argument("--dry-run", action="store_true", help="rank layout only: gloo on the CPU, no GPU")
     ap.add_argument("--no-other", action="store_true", help="skip the C4 / C5 kernel figures (one GPU only)")
+    ap.add_argument("--slice-of", type=int, default=0,
+                    help="one GPU: encode rank 0's byte range of an N-rank split (the launch shape each rank of an "
+                         "N-GPU run has, for its rocprofv3 PMC passes); not a job-throughput figure")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -263,7 +285,11 @@ def main():
 
     K, P, S = WORKLOADS[args.workload]
     B = args.stripes
-    if args.split == "bytes":
+    if args.slice_of > 1:
+        if world != 1:
+            raise SystemExit("--slice-of is a one-GPU measurement")
+        lo, hi = rsd.byte_range(S, 0, args.slice_of)
+    elif args.split == "bytes":
         lo, hi = rsd.byte_range(S, rank, world)
     else:
         lo, hi = 0, S
@@ -320,11 +346,13 @@ def main():
         _, one_ms = timed(slab[:1], max(50, args.steps))
 
     t = torch.tensor([el, kern_ms, one_ms or 0.0, flat_ms or 0.0], dtype=torch.float64, device=dev)
-    per_rank = [kern_ms]
+    per_rank, per_rank_w = [kern_ms], [W]
     if world > 1:
-        allk = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
-        dist.all_gather(allk, t[1:2].clone())
-        per_rank = [float(x) for x in allk]
+        mine = torch.tensor([kern_ms, float(W)], dtype=torch.float64, device=dev)
+        allk = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(allk, mine)
+        per_rank = [float(x[0]) for x in allk]
+        per_rank_w = [int(x[1]) for x in allk]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el, kern_ms, one_ms, flat_ms = float(t[0]), float(t[1]), float(t[2]) or None, float(t[3]) or None
 
@@ -341,6 +369,8 @@ def main():
     alg_bytes = B * (K + P) * W  # per launch on one rank
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     kname = codec.encode_path
+    # each rank's algorithmic bytes over its own kernel time
+    per_rank_frac = [B * (K + P) * w_r / (k_ms * 1e-3) / 1e9 / PEAK_HBM_GBS for k_ms, w_r in zip(per_rank, per_rank_w)]
 
     if rank == 0:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
@@ -364,8 +394,11 @@ def main():
                 "data_shards": K,
                 "parity_shards": P,
                 "shard_bytes": S,
-                "parallelism": (f"byte-range split over {world} rank(s): {W} bytes of every row per rank"
+                "parallelism": (f"one GPU running rank 0's slice of a {args.slice_of}-rank byte-range split: {W} bytes of every row"
+                                if args.slice_of > 1 else
+                                f"byte-range split over {world} rank(s): {W} bytes of every row per rank"
                                 if args.split == "bytes" else f"independent stripes, {world} rank(s)"),
+                "row_bytes_per_rank": W,
                 "kernel_path": kname,
                 "layout": f"rows at a stride of {W} + {pad} bytes, stripes back to back",
             },
@@ -379,10 +412,15 @@ def main():
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
-                "traffic": load_traffic(kname, args.workload, B) if world == 1 else None,
+                # HBM bytes of one launch of this rank's shape (its stripes x
+                # its row slice), from the committed PMC passes of that shape
+                "traffic": load_traffic(kname, args.workload, B, W, S),
+                "traffic_key": traffic_key(args.workload, kname, B, W),
                 "kernel_ms": round(kern_ms, 5),
                 "alg_bytes_per_launch": alg_bytes,
             },
+            "per_rank_frac": [round(f, 4) for f in per_rank_frac],
+            "per_rank_row_bytes": per_rank_w,
             "unpadded_rows": None if flat_ms is None else {
                 "kernel_ms": round(flat_ms, 5),
                 "frac": round(alg_bytes / (flat_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
@@ -391,11 +429,13 @@ def main():
                 "kernel_ms": round(one_ms, 5),
                 "frac": round((K + P) * W / (one_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
             },
-            "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(K, P, S, args.cpu_seconds, threads),
+            # rank 0 only, after the timed region (the other ranks wait at the barrier below)
+            "cpu_baseline": None if args.no_cpu else cpu_baseline(K, P, S, args.cpu_seconds, threads),
             "other_workloads": other,
         }
         print(json.dumps(res), flush=True)
     if world > 1:
+        dist.barrier(device_ids=[dev.index])
         dist.destroy_process_group()
 
 

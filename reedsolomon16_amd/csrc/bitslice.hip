@@ -19,9 +19,9 @@
 // same 8x8 GF(2) map on both byte halves of a symbol.  So a lane holds one
 // half (8 bit-planes) of a 64-byte block, and the half becomes a lane bit.
 //
-// Work split: two (m = 32) or four (m = 16) independent 256-thread
-// workgroups per CU, persistent over tiles.  A tile is 2 KB (32 blocks) of
-// every row of one stripe; lane l = (block l & 31, half l >> 5) in each of
+// Work split: one 2 KB tile (32 blocks of every row of one stripe) per
+// 256-thread workgroup, two (m = 32) or four (m = 16) workgroups resident per
+// CU; lane l = (block l & 31, half l >> 5) in each of
 // the 4 waves.  With RW = m/4 rows per wave and LR = LOGM - 2:
 //
 //   chunk IFFT layers r0 .. r(LR-1) (leopard16.go:694-741): wave w holds rows
@@ -74,9 +74,6 @@ static_assert(fft_slot(4, 3, 0) == 1 && fft_slot(4, 2, 8) == 2 && fft_slot(4, 0,
 // x ^= y * twiddle (C >= 0: chunk C's IFFT slot; C < 0: FFT slot)
 template <class TW, int C, int SLOT>
 __device__ __forceinline__ void hp_mul_add(Half &x, const Half &y) {
-#ifdef RS_BS_ABL_NOMUL  // ablation (performance experiments only)
-    return;
-#endif
 #pragma unroll
     for (int i = 0; i < 8; i++) xor_net8(x[i], y, C < 0 ? TW::fft8[SLOT][i] : TW::ifft8[C < 0 ? 0 : C][SLOT][i]);
 }
@@ -136,19 +133,11 @@ __device__ __forceinline__ uint32_t hp_row_addr(uint32_t lbase, int row) {
     return b + (uint32_t)row * 2048u;
 }
 __device__ __forceinline__ void hp_put(uint32_t lbase, int row, const Half &v) {
-#ifdef RS_BS_ABL_NOLDS
-    return;
-#endif
     const uint32_t ra = hp_row_addr(lbase, row);
     *(lds_u4 *)(uintptr_t)ra = u32x4{v[0], v[1], v[2], v[3]};
     *(lds_u4 *)(uintptr_t)(ra + 1024) = u32x4{v[4], v[5], v[6], v[7]};
 }
 __device__ __forceinline__ void hp_get(uint32_t lbase, int row, Half &v) {
-#ifdef RS_BS_ABL_NOLDS
-#pragma unroll
-    for (int q = 0; q < 8; q++) asm volatile("" : "+v"(v[q]));
-    return;
-#endif
     const uint32_t ra = hp_row_addr(lbase, row);
     const u32x4 x = *(const lds_u4 *)(uintptr_t)ra;
     const u32x4 y = *(const lds_u4 *)(uintptr_t)(ra + 1024);
@@ -170,10 +159,7 @@ struct HpEncoder {
     static constexpr int U = M / 16;       // cosets per wave
     static constexpr int NCH = TW::NCH;    // chunks compiled in (k <= NCH * m)
     static constexpr int TILE = 2048;      // column bytes per tile (32 blocks)
-#ifndef RS_HP_PF1  // rows of the next chunk issued before phase 1 (m = 32)
-#define RS_HP_PF1 2
-#endif
-    static constexpr int PF1 = LOGM == 5 ? RS_HP_PF1 : HR / 2;
+    static constexpr int PF1 = LOGM == 5 ? 2 : HR / 2;  // rows of the next chunk issued before phase 1
     static_assert(LOGM == 4 || LOGM == 5, "m = 16 or 32");
     const BsArgs &a;
     uint32_t lbase;  // this lane's LDS byte address of row 0, quad 0
@@ -201,11 +187,7 @@ struct HpEncoder {
     // the next row; their results are never stored.
     template <int I0, int I1>
     __device__ __forceinline__ void stage(const Loc &L, int c) {
-#ifdef RS_BS_ABL_NOLOAD
-        const uint32_t range = 0;
-#else
         const uint32_t range = L.live ? a.span : 0u;
-#endif
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(a.data + (L.live ? (uint64_t)L.stripe * a.stripe_stride : 0)), 0, (int)range, 0x00020000);
         // lane part of the offset (block, half); opaque so that the compiler
@@ -383,11 +365,7 @@ struct HpEncoder {
                             const u32x4 old = __builtin_amdgcn_raw_buffer_load_b128(ps, voff + k * QS, soff, 0);
                             bad |= (old[0] ^ v[0]) | (old[1] ^ v[1]) | (old[2] ^ v[2]) | (old[3] ^ v[3]);
                         } else {
-#if defined(RS_BS_ABL_NOSTORE)
-                            asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
-#else
                             __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * QS, soff, 0);
-#endif
                         }
                     }
                 }
@@ -432,12 +410,9 @@ hipError_t launch_hp_t(bool verify, BsArgs a, int cus, hipStream_t s) {
     // one finishes, so the loads of starting tiles overlap the stores of
     // finishing ones without the persistent grid's lockstep (same-box A/B,
     // 128 C3 stripes: 4.39 -> 4.25 ms, 0.611 -> 0.631 of the HBM roofline,
-    // scripts/gpu_hpgrid.sh).  RS_HP_GRID=n (A/B only): persistent, n per CU.
-    static const int gmode = [] {
-        const char *e = getenv("RS_HP_GRID");
-        return e ? atoi(e) : 0;
-    }();
-    const int grid = gmode <= 0 ? a.ntiles : std::min(a.ntiles, gmode * cus);
+    // profiles/r03_c3_grid_ab.txt).
+    const int grid = a.ntiles;
+    (void)cus;
     if (verify) hipLaunchKernelGGL((k_encode_hp<LOGM, true>), dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_encode_hp<LOGM, false>), dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();

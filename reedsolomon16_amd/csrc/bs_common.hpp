@@ -109,9 +109,6 @@ __device__ __forceinline__ void bs_xchg(uint32_t &a, uint32_t &b, int s, uint32_
 // of symbol 4w + j) <-> 8 bit-planes (plane b bit 8j + w = bit b of symbol
 // 4w + j).  Three delta-swap stages; an involution.
 __device__ __forceinline__ void bs_transpose8(Half &w) {
-#ifdef RS_BS_ABL_NOTRANS
-    return;
-#endif
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const int s = 1 << k;

@@ -317,36 +317,25 @@ int upload_split(rs_codec *c) {
     return RS_OK;
 }
 
-// RS_BS=0 disables the bit-sliced kernel (A/B experiments only).
-bool bs_enabled() {
-    const char *e = getenv("RS_BS");
-    return !(e && e[0] == '0');
+// Test-only path overrides.  The parity tests use them to run the kernel
+// variants that other geometries select (the bit-sliced encode off, the
+// transforms in full-field coordinates, the reconstruct FFT unpruned) on the
+// same small inputs; nothing else reads them.  (kernels.hip unit_width_override
+// is the fourth: RS_UNIT_WIDTH.)
+bool env_flag(const char *name, char on) {
+    const char *e = getenv(name);
+    return e && e[0] == on;
 }
-
-// RS_NO_SUB=1 disables subfield-coordinate transforms (A/B experiments only).
-bool sub_enabled() {
-    const char *e = getenv("RS_NO_SUB");
-    return !(e && e[0] == '1');
-}
-
-// RS_NO_PRUNE=1 disables the FFT group pruning of the LDS reconstruct (A/B experiments only).
-bool prune_enabled() {
-    const char *e = getenv("RS_NO_PRUNE");
-    return !(e && e[0] == '1');
-}
-
-// RS_NO_SPLIT=1 disables the split kernel (A/B experiments only).
-bool split_enabled() {
-    const char *e = getenv("RS_NO_SPLIT");
-    return !(e && e[0] == '1');
-}
+bool bs_enabled() { return !env_flag("RS_BS", '0'); }           // RS_BS=0: no bit-sliced encode
+bool sub_enabled() { return !env_flag("RS_NO_SUB", '1'); }      // RS_NO_SUB=1: full-field coordinates
+bool prune_enabled() { return !env_flag("RS_NO_PRUNE", '1'); }  // RS_NO_PRUNE=1: unpruned reconstruct FFT
 
 // Host half of the encode plan (no device calls): twiddle schedule and panic check.
 void plan_encode_host(rs_codec *c) {
     c->enc_ok = encode_schedule(*c->F, c->k, c->p, c->enc_ifft_logs, c->enc_fft_logs, c->nchunks);
     c->path = !c->enc_ok ? "panic" : (c->logm <= kMaxRegLogM ? encode_reg_name(c->bits, c->logm)
                                                    : c->logm <= kMaxLdsLogN ? "lds-m" + std::to_string(c->m) : "multipass");
-    if (c->enc_ok && c->bits == 16 && c->logm >= 2 && c->logm <= 5 && split_enabled())
+    if (c->enc_ok && c->bits == 16 && c->logm >= 2 && c->logm <= 5)
         c->path = std::string("split16-m") + std::to_string(c->m);
     c->bs_ok = c->enc_ok && c->bits == 16 && (c->logm == 4 || c->logm == 5) && bs_enabled() &&
                encode_bs_available(c->k, c->p, c->enc_ifft_logs.data(), c->enc_fft_logs.data(), c->F->mod);
@@ -366,7 +355,7 @@ int ensure_device(rs_codec *c) {
         if (e) return e;
         e = upload_twiddles(c, c->enc_fft_logs, c->tw_fft);
         if (e) return e;
-        if (c->bits == 16 && split_enabled()) {
+        if (c->bits == 16) {
             e = upload_split(c);
             if (e) return e;
         }
@@ -425,12 +414,8 @@ hipStream_t pick_stream(rs_codec *c, void *s) {
 // (nothing to do when that was this stream: it is in order already, and an
 // explicit wait would stop the next launch from being queued behind the
 // previous one).
-bool scratch_wait_same_stream() {
-    const char *e = getenv("RS_SCRATCH_SAME_STREAM");  // "wait": A/B experiments only
-    return e && e[0] == 'w';
-}
 int scratch_acquire(rs_codec *c, hipStream_t s) {
-    if (c->scratch_used && (s != c->scratch_stream || scratch_wait_same_stream()))
+    if (c->scratch_used && s != c->scratch_stream)
         HIP_TRY(hipStreamWaitEvent(s, c->scratch_ev, 0));
     return RS_OK;
 }

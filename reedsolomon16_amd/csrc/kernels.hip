@@ -24,56 +24,6 @@
 #include "rec_common.hpp"
 #include "schedule.hpp"
 
-// Performance-experiment knobs (scripts/ablate.sh builds separate libraries
-// with these; the product build defines none of them):
-//   RS_ABL_NO_DMA      fused encode: skip the HBM->LDS staging (computes on stale LDS)
-//   RS_ABL_ONE_TW      fused encode: every butterfly uses twiddle slot 0
-//   RS_ABL_NO_MUL      fused encode: butterflies are XOR-only
-#ifndef RS_ABL_NO_DMA
-#define RS_ABL_NO_DMA 0
-#endif
-#ifndef RS_ABL_ONE_TW
-#define RS_ABL_ONE_TW 0
-#endif
-#ifndef RS_ABL_NO_MUL
-#define RS_ABL_NO_MUL 0
-#endif
-// RS_ABL_TAB_ONCE: fused encode reads one twiddle table per transform (wrong results)
-// RS_ABL_NOSWAP: split kernel skips its permlane32 swaps (wrong results)
-#ifndef RS_ABL_NOSWAP
-#define RS_ABL_NOSWAP 0
-#endif
-#ifndef RS_ABL_TAB_ONCE
-#define RS_ABL_TAB_ONCE 0
-#endif
-// RS_STAMP: fused encode records per-wave (s_memtime, s_memrealtime) deltas in
-// g_rs_stamps (diagnostic builds only: scripts/micro/encode_lab.hip)
-#ifndef RS_STAMP
-#define RS_STAMP 0
-#endif
-#if RS_STAMP
-__device__ unsigned long long g_rs_stamps[3 << 16];
-#endif
-// RS_OP_FENCE: scheduling fence after every butterfly op of the fused kernels.
-#ifndef RS_OP_FENCE
-#define RS_OP_FENCE 0
-#endif
-// RS_OP_PIN: chain every butterfly op's outputs with an empty asm (bounds code motion).
-#ifndef RS_ABL_IFFT_AS_FFT
-#define RS_ABL_IFFT_AS_FFT 0  // timing experiment only: run the FFT op list per chunk (wrong result)
-#endif
-#ifndef RS_SPLIT_PREQ
-#define RS_SPLIT_PREQ 3  // quads (of 5) of the next twiddle table prefetched by the split kernel
-#endif
-#ifndef RS_SPLIT_PIN
-#define RS_SPLIT_PIN 1
-#endif
-#ifndef RS_DMA_SPREAD
-#define RS_DMA_SPREAD 1
-#endif
-#ifndef RS_OP_PIN
-#define RS_OP_PIN 1
-#endif
 
 namespace rs {
 namespace {
@@ -312,11 +262,7 @@ struct F16S : F16<W_> {
 };
 
 // ---------------------------------------------------------------- butterflies
-#ifdef RS_LDS_ABL_NOMUL  // ablation (performance experiments only): table-driven butterflies are XOR-only
-#define RS_TW_LIVE(t) false
-#else
 #define RS_TW_LIVE(t) ((t)[F::LOGIDX] != F::MOD)
-#endif
 template <class F>
 __device__ __forceinline__ void ifft2(typename F::Vec &x, typename F::Vec &y, const uint32_t *__restrict__ t) {
     F::xor_into(y, x);
@@ -489,24 +435,22 @@ __device__ __forceinline__ void run_ops(typename F::Vec *w, uint32_t ltab, const
     constexpr int NT = runs.count;
     constexpr int TB = F::TWD * 4;  // bytes per table slot
     Tab<F> t0, t1;
-    if constexpr (NT > 0) t0 = lds_tab<F>(ltab, (RS_ABL_ONE_TW ? 0 : runs.slot[0]) * TB);
+    if constexpr (NT > 0) t0 = lds_tab<F>(ltab, runs.slot[0] * TB);
     int have = 0;  // index of the table in t0
 #pragma unroll
     for (int i = 0; i < N; i++) {
         const BOp o = ops.op[i];
         const int need = runs.first_use[i];
         hook(i);
-        if (!RS_ABL_TAB_ONCE && need >= 0 && need != have) {  // next run: its table was prefetched into t1
+        if (need >= 0 && need != have) {  // next run: its table was prefetched into t1
             t0 = t1;
             have = need;
         }
-        if (!RS_ABL_TAB_ONCE && need >= 0 && (i == 0 || runs.first_use[i - 1] != need)) {
-            if (have + 1 < NT) t1 = lds_tab<F>(ltab, (RS_ABL_ONE_TW ? 0 : runs.slot[have + 1 < NT ? have + 1 : 0]) * TB);
+        if (need >= 0 && (i == 0 || runs.first_use[i - 1] != need)) {
+            if (have + 1 < NT) t1 = lds_tab<F>(ltab, runs.slot[have + 1 < NT ? have + 1 : 0] * TB);
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (RS_ABL_NO_MUL) {
-            F::xor_into(w[o.y], w[o.x]);
-        } else if (o.kind == OP_IFFT) {
+        if (o.kind == OP_IFFT) {
             F::xor_into(w[o.y], w[o.x]);
             F::mul_add(w[o.x], w[o.y], t0.v);
         } else if (o.kind == OP_FFT) {
@@ -515,13 +459,8 @@ __device__ __forceinline__ void run_ops(typename F::Vec *w, uint32_t ltab, const
         } else {
             F::xor_into(w[o.y], w[o.x]);
         }
-#if RS_OP_PIN
-        F::pin(w[o.x]);
+        F::pin(w[o.x]);  // chain every op's outputs: bounds code motion
         F::pin(w[o.y]);
-#endif
-#if RS_OP_FENCE
-        __builtin_amdgcn_sched_barrier(0);
-#endif
     }
 }
 
@@ -615,8 +554,7 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
             const int P = j * 64 + lane;
             const int r = P / PPR;
             const uint64_t go = span + F::piece_goff(P % PPR);
-            if (RS_ABL_NO_DMA) {
-            } else if (wave_live && r < cnt && go < a.shard_size) {
+            if (wave_live && r < cnt && go < a.shard_size) {
                 if constexpr (TABLE) {
                     const uint8_t *src = rowp<TABLE>(a.data, row0 + r, soff) + go;
                     __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(img + j * 1024), 16, 0, 0);
@@ -648,28 +586,12 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
         }
     };
 
-#if RS_STAMP
-    const unsigned long long st_c0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
     V acc[M];
     stage(0);
     stage_tab(a.tw_ifft, IS, 0);
-#if RS_STAMP
-    unsigned long long st_wait = 0, st_first = 0;
-#endif
     for (int c = 0; c < a.nchunks; ++c) {
-#if RS_STAMP
-        const unsigned long long sw0 = __builtin_amdgcn_s_memtime();
-#endif
         wait_vm0();  // this wave's DMAs for chunk c have landed
         __syncthreads();  // every wave's table pieces landed; buffer (c+1)&1 is no longer read
-#if RS_STAMP
-        {
-            const unsigned long long sw1 = __builtin_amdgcn_s_memtime();
-            if (c == 0) st_first = sw1 - st_c0;
-            else st_wait += sw1 - sw0;
-        }
-#endif
         V cur[M];
 #pragma unroll
         for (int r = 0; r < M; r++) cur[r] = F::lds_load(img + r * ROWB, lane);
@@ -681,16 +603,11 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
         // every SPREAD ops): issued back to back while the whole GPU streams,
         // they stall the wave at issue before any butterfly starts.
         constexpr int NOPS = ifft_op_count<LOGM>();
-        constexpr int SPREAD = (RS_DMA_SPREAD && NOPS >= NDMA) ? NOPS / NDMA : 0;
+        constexpr int SPREAD = NOPS >= NDMA ? NOPS / NDMA : 0;
         if (!SPREAD && more) stage(c + 1);
-        if (RS_ABL_IFFT_AS_FFT) {
-            if (more) stage(c + 1);
-            fft_reg<F, LOGM>(cur, vgpr_lds_addr(ltab + (c & 1) * TABB));
-        } else {
-            ifft_reg<F, LOGM>(cur, vgpr_lds_addr(ltab + (c & 1) * TABB), [&](int i) {
-                if (SPREAD && i % SPREAD == 0 && i / SPREAD < NDMA && more) stage_one(c + 1, i / SPREAD);
-            });
-        }
+        ifft_reg<F, LOGM>(cur, vgpr_lds_addr(ltab + (c & 1) * TABB), [&](int i) {
+            if (SPREAD && i % SPREAD == 0 && i / SPREAD < NDMA && more) stage_one(c + 1, i / SPREAD);
+        });
         if (c == 0) {
 #pragma unroll
             for (int r = 0; r < M; r++) acc[r] = cur[r];
@@ -698,51 +615,10 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
 #pragma unroll
             for (int r = 0; r < M; r++) F::xor_into(acc[r], cur[r]);
         }
-#if RS_STAMP
-        if (lane == 0 && blockIdx.y == 0 && c < 8) {
-            const unsigned i3 = (blockIdx.x * 4 + wave) * 16 + 2 * c + 65536;
-            if (i3 + 1 < 3u * 65536) {
-                g_rs_stamps[i3] = __builtin_amdgcn_s_memtime() - sw0;  // whole chunk incl. wait
-                g_rs_stamps[i3 + 1] = sw0 - st_c0;                      // chunk start
-            }
-        }
-#endif
     }
-#if RS_STAMP
-    const unsigned long long sf0 = __builtin_amdgcn_s_memtime();
-#endif
     wait_vm0();
     __syncthreads();
-#if RS_STAMP
-    const unsigned long long sf1 = __builtin_amdgcn_s_memtime();
-#endif
     fft_reg<F, LOGM>(acc, vgpr_lds_addr(ltab + (a.nchunks & 1) * TABB));
-#if RS_STAMP
-    const unsigned long long sf2 = __builtin_amdgcn_s_memtime();
-    if (lane == 0 && blockIdx.y == 0) {
-        const unsigned i2 = (blockIdx.x * 4 + wave) * 4 + 32768;
-        if (i2 + 3 < (1u << 16)) {
-            g_rs_stamps[i2] = st_first;
-            g_rs_stamps[i2 + 1] = st_wait + (sf1 - sf0);
-            g_rs_stamps[i2 + 2] = sf2 - sf1;
-            g_rs_stamps[i2 + 3] = sf0 - st_c0;
-        }
-    }
-    if (lane == 0 && blockIdx.y == 0) {
-        const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        const unsigned idx = (blockIdx.x * 4 + wave) * 4;
-        if (idx + 3 < (1u << 16)) {
-            g_rs_stamps[idx] = c1 - st_c0;
-            g_rs_stamps[idx + 1] = r1 - st_r0;
-            g_rs_stamps[idx + 2] = st_r0;
-            unsigned xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            unsigned hw;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            g_rs_stamps[idx + 3] = ((unsigned long long)xcc << 32) | hw;
-        }
-    }
-#endif
     if (!wave_live || u >= units) return;
     if constexpr (VERIFY) {
         uint32_t bad = 0;
@@ -783,17 +659,14 @@ __device__ __forceinline__ void run_split(F16<1>::Vec *w, uint32_t ltab) {
     constexpr int NT = sch.ntab;
     constexpr int TB = F::TWD * 4;
     constexpr int NQ = (F::TWU + 3) / 4;              // quads per table
-    constexpr int PQ = RS_SPLIT_PREQ < NQ ? RS_SPLIT_PREQ : NQ;  // quads of the next table prefetched
+    constexpr int PQ = 3 < NQ ? 3 : NQ;  // quads (of 5) of the next table prefetched
     Tab<F> t0, t1;
     if constexpr (NT > 0) lds_tab_part<F>(t0, ltab, 0, 0, NQ);
     int have = 0;
-    int opi = 0;
-    (void)opi;
 #pragma unroll
     for (int i = 0; i < NS; i++) {
         const SStep st = sch.step[i];
         if (st.type == ST_SWAP) {
-            if (RS_ABL_NOSWAP) continue;
             const auto rl = __builtin_amdgcn_permlane32_swap(w[st.a].l[0], w[st.b].l[0], false, false);
             const auto rh = __builtin_amdgcn_permlane32_swap(w[st.a].h[0], w[st.b].h[0], false, false);
             w[st.a].l[0] = rl[0];
@@ -802,7 +675,7 @@ __device__ __forceinline__ void run_split(F16<1>::Vec *w, uint32_t ltab) {
             w[st.b].h[0] = rh[1];
             continue;
         }
-        const int need = RS_ABL_TAB_ONCE ? (st.tab >= 0 ? 0 : -1) : st.tab;
+        const int need = st.tab;
         if (need >= 0 && need != have) {  // next table run: its first PQ quads were prefetched into t1
 #pragma unroll
             for (int j = 0; j < 4 * PQ && j < F::TWU; j++) t0.v[j] = t1.v[j];
@@ -819,9 +692,7 @@ __device__ __forceinline__ void run_split(F16<1>::Vec *w, uint32_t ltab) {
             __builtin_amdgcn_sched_barrier(0);
         }
         typename F::Vec &x = w[st.a], &y = w[st.b];
-        if (RS_ABL_NO_MUL) {
-            F::xor_into(y, x);
-        } else if (st.kind == OP_IFFT) {
+        if (st.kind == OP_IFFT) {
             F::xor_into(y, x);
             F::mul_add(x, y, t0.v);
         } else if (st.kind == OP_FFT) {
@@ -830,14 +701,9 @@ __device__ __forceinline__ void run_split(F16<1>::Vec *w, uint32_t ltab) {
         } else {
             F::xor_into(y, x);
         }
-#if RS_SPLIT_PIN
-        // pin every RS_SPLIT_PIN-th op: bounds code motion (VGPRs) while letting
-        // consecutive independent butterflies interleave
-        if ((opi++ % RS_SPLIT_PIN) == RS_SPLIT_PIN - 1) {
-            F::pin(x);
-            F::pin(y);
-        }
-#endif
+        // pin every op: bounds code motion (VGPRs)
+        F::pin(x);
+        F::pin(y);
     }
 }
 
@@ -889,7 +755,6 @@ __global__ void __launch_bounds__(256, 4) k_encode_split(EncodeArgs a) {
     const uint32_t lane_off = (uint32_t)((lane >> 4) * a.data.stride) + (lane & 15) * 16 + span;
     auto stage_one = [&](int c, int j) {
         const int row0 = c * M, cnt = a.k - row0;
-        if (RS_ABL_NO_DMA) return;
         if (wave_full && cnt >= M) {
             const uint32_t so = (uint32_t)((uint64_t)(row0 + 4 * j) * a.data.stride);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(drsrc, (lvoid_t *)(img + j * 1024), 16, lane_off, so, 0, 0);
@@ -916,11 +781,6 @@ __global__ void __launch_bounds__(256, 4) k_encode_split(EncodeArgs a) {
     };
     constexpr int IMGB = 2 * NTI * TB, FMGB = 2 * NTF * TB;  // bytes of one chunk's / the FFT's table image
 
-#if RS_STAMP
-    const unsigned long long st_c0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long st_first = 0, st_wait = 0;
-    const unsigned swave = blockIdx.x * 4 + wave;
-#endif
     V acc[HM];
 #pragma unroll
     for (int j = 0; j < NDMA; j++) stage_one(0, j);
@@ -928,18 +788,8 @@ __global__ void __launch_bounds__(256, 4) k_encode_split(EncodeArgs a) {
     // lane's LDS read base: register k holds row row0[k] (lower) / row0[k] | 1 << H0 (upper)
     const uint8_t *rd = img + half * ((1 << H0) * ROWB) + colb;
     for (int c = 0; c < a.nchunks; ++c) {
-#if RS_STAMP
-        const unsigned long long sw0 = __builtin_amdgcn_s_memtime();
-#endif
         wait_vm0();
         __syncthreads();
-#if RS_STAMP
-        {
-            const unsigned long long sw1 = __builtin_amdgcn_s_memtime();
-            if (c == 0) st_first = sw1 - st_c0;
-            else st_wait += sw1 - sw0;
-        }
-#endif
         V cur[HM];
 #pragma unroll
         for (int k = 0; k < HM; k++) {
@@ -963,38 +813,10 @@ __global__ void __launch_bounds__(256, 4) k_encode_split(EncodeArgs a) {
 #pragma unroll
             for (int k = 0; k < HM; k++) F::xor_into(acc[k], cur[k]);
         }
-#if RS_STAMP
-        if (lane == 0 && blockIdx.y == 0 && c < 8 && swave < 8192) {
-            g_rs_stamps[65536 + 16 * swave + 2 * c] = __builtin_amdgcn_s_memtime() - sw0;
-            g_rs_stamps[65536 + 16 * swave + 2 * c + 1] = sw0 - st_c0;
-        }
-#endif
     }
-#if RS_STAMP
-    const unsigned long long sf0 = __builtin_amdgcn_s_memtime();
-#endif
     wait_vm0();
     __syncthreads();
-#if RS_STAMP
-    const unsigned long long sf1 = __builtin_amdgcn_s_memtime();
-#endif
     run_split<FftSplit<LOGM>>(acc, vgpr_lds_addr(ltab + (a.nchunks & 1) * TABB) + (uint32_t)half * (NTF * TB));
-#if RS_STAMP
-    if (lane == 0 && blockIdx.y == 0 && swave < 8192) {
-        const unsigned long long sf2 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        g_rs_stamps[32768 + 4 * swave] = st_first;
-        g_rs_stamps[32768 + 4 * swave + 1] = st_wait + (sf1 - sf0);
-        g_rs_stamps[32768 + 4 * swave + 2] = sf2 - sf1;
-        g_rs_stamps[32768 + 4 * swave + 3] = sf0 - st_c0;
-        g_rs_stamps[4 * swave] = sf2 - st_c0;
-        g_rs_stamps[4 * swave + 1] = r1 - st_r0;
-        g_rs_stamps[4 * swave + 2] = st_r0;
-        unsigned xcc, hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        g_rs_stamps[4 * swave + 3] = ((unsigned long long)xcc << 32) | hw;
-    }
-#endif
     if (!lane_live) return;
     // register k, half h holds parity row fin_row[h][k]; the two halves' rows differ by 1 << HF
     const uint64_t prow_step = (uint64_t)a.parity.stride;
@@ -1197,26 +1019,9 @@ hipError_t enc_reg(bool verify, const EncodeArgs &a, hipStream_t s) {
 // tile must cover whole 64-byte blocks (low bytes [0,32), high bytes
 // [32,64)), so W = 1 (32-byte tiles) is invalid: the parity tests reject it.
 constexpr uint64_t kLdsMinGrid = 512;
-#ifndef RS_ENC_ACC_REGS
-#define RS_ENC_ACC_REGS 1  // k_enc_lds keeps the accumulator in registers (even log m); 0: in LDS
-#endif
-#ifndef RS_ENC_LDS_MINBLK
-#define RS_ENC_LDS_MINBLK 4  // k_enc_lds occupancy hint (workgroups per CU): 4 = <= 128 VGPRs
-#endif
-constexpr bool enc_acc_regs(int logm) { return RS_ENC_ACC_REGS && logm % 2 == 0 && logm >= 4; }
-#ifndef RS_REC_NO_ZSKIP
-#define RS_REC_NO_ZSKIP 0  // 1: the from-HBM IFFT pass transforms the all-zero groups past mtrunc too (A/B)
-#endif
-#ifndef RS_REC_UNFUSED_DERIV
-#define RS_REC_UNFUSED_DERIV 0  // 1: formal derivative as its own LDS pass (A/B experiments)
-#endif
-#ifndef RS_LDS_BRANCHFREE
-#define RS_LDS_BRANCHFREE 1
-#endif
-constexpr bool kLdsBranchFree = RS_LDS_BRANCHFREE;  // lane-varying passes: branch-free multiplies
-#ifndef RS_LDS_PAD
-#define RS_LDS_PAD 16  // LDS row padding of the LDS-resident kernels (bytes)
-#endif
+// k_enc_lds keeps the accumulator in registers for even log m
+constexpr bool enc_acc_regs(int logm) { return logm % 2 == 0 && logm >= 4; }
+constexpr bool kLdsBranchFree = 1;  // lane-varying passes: branch-free multiplies
 
 // RS_UNIT_WIDTH=wide / narrow forces the per-launch unit-width choices below
 // (LDS tiles of 128 vs 64 bytes; GF(2^8) register units of 16 vs 4 bytes) so
@@ -1236,7 +1041,7 @@ struct LTile {
     static_assert(!F::SYM16 || F::W >= 2, "a GF(2^16) LDS tile must cover whole 64-byte blocks (W >= 2)");
     static constexpr bool W16 = F::SYM16;
     static constexpr int TB = 32 * F::W;                  // bytes of each row owned by a workgroup
-    static constexpr int ROW = TB + RS_LDS_PAD;  // LDS row stride
+    static constexpr int ROW = TB + 16;  // LDS row stride (16 bytes of padding)
     static constexpr int UB = W16 ? 8 * F::W : 4 * F::W;  // global bytes per unit
     static constexpr int U = TB / UB;                     // units per tile
     typedef typename F::Vec V;
@@ -1334,7 +1139,6 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
             out(i + 2 * dist, u, x2);
             out(i + 3 * dist, u, x3);
         };
-#ifndef RS_LDS_VECTOR_TW
         if (dist * U >= 64) {
             // A wave's 64 items (aligned) lie in one group: the group index is
             // wave-uniform, so its twiddle tables come in by scalar loads and
@@ -1342,7 +1146,6 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
             for (int it = threadIdx.x; it < items; it += 256)
                 group(it, __builtin_amdgcn_readfirstlane((it / U) >> ld), std::false_type{});
         } else
-#endif
         {
             for (int it = threadIdx.x; it < items; it += 256) group(it, (it / U) >> ld, std::bool_constant<kLdsBranchFree>{});
         }
@@ -1361,9 +1164,7 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
             out(ry, u, y);
         }
     }
-#ifndef RS_LDS_ABL_NOBAR  // ablation: wrong results, measures the barrier cost
     lds_sync();
-#endif
 }
 
 // Full transform over 2^LOGN LDS rows with the reference's pass structure
@@ -1394,7 +1195,7 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
         if constexpr (radix4) {
             active = (mtrunc + 4 * dist - 1) / (4 * dist);
             if (active > groups) active = groups;
-            if constexpr (from_hbm && INV && p < NP - 1 && !RS_REC_NO_ZSKIP) {
+            if constexpr (from_hbm && INV && p < NP - 1) {
                 // groups past mtrunc hold zero rows: zero their LDS rows instead
                 // of transforming them (the pass's barrier covers these stores)
                 const int z0 = active * 4 * dist;
@@ -1479,7 +1280,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
     const Reveal rv{a, tile, sbase, load_need(a.need)};
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
-    if constexpr (LOGN >= 3 && !RS_REC_UNFUSED_DERIV) {
+    if constexpr (LOGN >= 3) {
         // fused with the FFT's first pass (radix-4 at dist D = N/4, one group,
         // twiddle slot 0): a thread forms the derivative of its four rows
         // i + aD from the IFFT image (the a-bit terms from the rows it holds),
@@ -1572,7 +1373,7 @@ __device__ __forceinline__ void sub_swap(typename F::Vec &v, const uint32_t *__r
 
 // FT: the field of the final FFT (F16S: subfield coordinates, EncodeArgs::tw_fft_sub).
 template <class F, int LOGM, bool VERIFY, class FT = F>
-__global__ void __launch_bounds__(256, RS_ENC_LDS_MINBLK) k_enc_lds(EncodeArgs a) {
+__global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
     constexpr int M = 1 << LOGM;
@@ -1905,16 +1706,8 @@ hipError_t rec_lds_w(int bits, int logn, bool sub, const RecArgs &a, hipStream_t
     if (bits != 16) return rec_lds_f<F8<W>>(logn, a, s);
     return sub ? rec_lds_f<F16<W>, F16S<W>>(logn, a, s) : rec_lds_f<F16<W>>(logn, a, s);
 }
-// RS_NO_BS_DEC=1 disables the bit-sliced n = 256 reconstruct (A/B experiments only).
-bool bs_dec_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("RS_NO_BS_DEC");
-        return !(e && e[0] == '1');
-    }();
-    return on;
-}
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s) {
-    if (bs_dec_enabled() && rec_bs256_available(bits, logn, sub, a.mtrunc)) return launch_rec_bs256(a, s);
+    if (rec_bs256_available(bits, logn, sub, a.mtrunc)) return launch_rec_bs256(a, s);
     const uint64_t ns = a.base && a.nstripes > 1 ? (uint64_t)a.nstripes : 1;
     const bool narrow = pick_narrow((a.S + 127) / 128 * ns < kLdsMinGrid);
     return narrow ? rec_lds_w<2>(bits, logn, sub, a, s) : rec_lds_w<4>(bits, logn, sub, a, s);

@@ -65,29 +65,43 @@ def main():
             r["Name"] = short(r["Name"])
             w.writerow(r)
 
+    # PMC passes: pmc_<COUNTER> (the bench's own shape) and pmc_<COUNTER>_s<N>
+    # (bench.py --slice-of N: rank 0's byte range of an N-rank split)
+    import sys
+    sys.path.insert(0, ROOT)
+    from reedsolomon16_amd.dist import byte_range
+
+    S = bench["config"]["shard_bytes"]
+    stripes = bench["config"].get("stripes_per_step", 16)
+    workload = bench["config"]["workload"].split(":")[0]
     agg = collections.defaultdict(list)
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        for fn in glob.glob(os.path.join(a.src, f"pmc_{c}", "run_counter_collection.csv")):
-            for r in csv.DictReader(open(fn)):
-                p = path_of(r["Kernel_Name"])
-                if p:
-                    agg[(p, r["Counter_Name"])].append(float(r["Counter_Value"]))
+        for d in glob.glob(os.path.join(a.src, f"pmc_{c}*")):
+            m = re.search(r"_s(\d+)$", d)
+            W = byte_range(S, 0, int(m.group(1)))[1] if m else bench["config"].get("row_bytes_per_rank", S)
+            for fn in glob.glob(os.path.join(d, "run_counter_collection.csv")):
+                for r in csv.DictReader(open(fn)):
+                    p = path_of(r["Kernel_Name"])
+                    if p:
+                        agg[(p, W, r["Counter_Name"])].append(float(r["Counter_Value"]))
     traffic, lines = {}, []
-    for p in sorted({k[0] for k in agg}):
-        fk = agg.get((p, "FETCH_SIZE"), [])
-        wk = agg.get((p, "WRITE_SIZE"), [])
+    for p, W in sorted({k[:2] for k in agg}):
+        fk = agg.get((p, W, "FETCH_SIZE"), [])
+        wk = agg.get((p, W, "WRITE_SIZE"), [])
         if not fk or not wk:
             continue
         fetch = sum(fk) / len(fk) * 1024
         write = sum(wk) / len(wk) * 1024
         hbm = 2 * fetch + write
-        traffic[p] = {"hbm_bytes_per_launch": round(hbm), "fetch_size_bytes": round(fetch),
-                      "write_size_bytes": round(write), "launches": len(fk),
-                      "stripes": bench["config"].get("stripes_per_step", 16),
-                      "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE = half of streamed reads)",
-                      "round": tag}
-        lines.append(f"{p}: FETCH_SIZE {fetch/1e6:.2f} MB (x2 = {2*fetch/1e6:.2f}), WRITE_SIZE {write/1e6:.2f} MB, "
-                     f"HBM {hbm/1e6:.2f} MB/launch over {len(fk)} launches")
+        alg = stripes * (bench["config"]["data_shards"] + bench["config"]["parity_shards"]) * W
+        traffic[f"{workload}:{p}:{stripes}x{W}"] = {
+            "hbm_bytes_per_launch": round(hbm), "fetch_size_bytes": round(fetch),
+            "write_size_bytes": round(write), "launches": len(fk), "stripes": stripes, "row_bytes": W,
+            "alg_bytes_per_launch": alg, "traffic_over_alg": round(hbm / alg, 4),
+            "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE = half of streamed reads)",
+            "round": tag}
+        lines.append(f"{p} {stripes}x{W}: FETCH_SIZE {fetch/1e6:.2f} MB (x2 = {2*fetch/1e6:.2f}), WRITE_SIZE "
+                     f"{write/1e6:.2f} MB, HBM {hbm/1e6:.2f} MB/launch ({hbm/alg:.4f} x algorithmic) over {len(fk)} launches")
     kern = [r for r in rows if "k_enc" in r["Name"] or "k_rec" in r["Name"]]
     for r in kern:
         lines.append(f"trace {short(r['Name'])}: calls {r['Calls']} avg {float(r['AverageNs'])/1e3:.2f} us "

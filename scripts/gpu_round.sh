@@ -21,5 +21,10 @@ rc=$?; echo "trace rc=$rc"; cat $OUT/trace_bench.json; [ $rc -eq 0 ] || exit $rc
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o run -- python3 bench.py --no-cpu --no-single --no-unpadded --no-other --steps 50 --warmup 5 > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  # the launch shape of each rank of an N-GPU byte-range run (bench.py --slice-of N)
+  for n in 2 4 8; do
+    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${c}_s$n -o run -- python3 bench.py --slice-of $n --no-cpu --no-single --no-unpadded --no-other --steps 50 --warmup 5 > $OUT/pmc_${c}_s$n.json 2> $OUT/pmc_${c}_s$n.err
+    rc=$?; echo "pmc $c slice $n rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  done
 done
 exit 0

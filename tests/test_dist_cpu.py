@@ -153,7 +153,8 @@ def test_bench_launcher_starts_n_ranks(gpus, workload):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(gpus), "--dry-run",
-                          "--workload", workload], capture_output=True, text=True, timeout=240, env=env, cwd=root)
+                          "--workload", workload, "--cpu-seconds", "0.4", "--cpu-threads", "2"],
+                         capture_output=True, text=True, timeout=240, env=env, cwd=root)
     assert out.returncode == 0, out.stderr[-2000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
@@ -164,6 +165,14 @@ def test_bench_launcher_starts_n_ranks(gpus, workload):
     S = {"C3": 1 << 20, "C5": 256 << 10}[workload]
     assert spans[0][0] == 0 and spans[-1][1] == S
     assert all(b == c for (_, b), (c, _) in zip(spans, spans[1:]))
+    # the N-rank line carries the 1-rank line's evidence: traffic keyed by each
+    # rank's launch shape, a per-rank roofline fraction, and the CPU baseline
+    assert "traffic" in res["roofline"] and len(res["roofline"]["per_rank_traffic"]) == gpus
+    for r in res["ranks"]:
+        assert r["traffic_key"].endswith("x%d" % (r["byte_range"][1] - r["byte_range"][0]))
+    assert len(res["per_rank_frac"]) == gpus
+    cb = res["cpu_baseline"]
+    assert cb["unit"] == "GiB/s" and cb["value"] > 0 and cb["kind"] == "port"
     # and a mismatched WORLD_SIZE is refused
     bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--dry-run"],
                          capture_output=True, text=True, timeout=120, env=dict(env, WORLD_SIZE="2", RANK="0"), cwd=root)
