@@ -70,71 +70,15 @@ using namespace bs;
 using namespace rec;
 
 typedef DecTab256 DT;
+typedef __attribute__((address_space(4))) const int ci32_t;
+typedef uint8_t *gptr_t;
+typedef __attribute__((address_space(4))) const gptr_t cptr_t;  // a row pointer held in read-only memory
+
 constexpr int kTile = 1024;      // column bytes per workgroup
 constexpr int kImgRows = 160;    // LDS image rows
 constexpr int kTw8 = 8;          // dwords per subfield twiddle table (kTwDwords8)
 constexpr int kTw16 = 24;        // dwords per full-field table (kTwDwords16)
 constexpr uint32_t kMod = 65535;
-
-// Tables, shard maps and row pointers are read through the constant address
-// space: read-only for the launch, so wave-uniform addresses become scalar loads.
-typedef __attribute__((address_space(4))) const uint32_t cu32_t;
-typedef __attribute__((address_space(4))) const int ci32_t;
-typedef uint8_t *gptr_t;
-typedef __attribute__((address_space(4))) const gptr_t cptr_t;  // a row pointer held in read-only memory
-__device__ __forceinline__ cu32_t *ctab(const uint32_t *t) { return (cu32_t *)t; }
-
-__device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
-    return __builtin_amdgcn_perm(s0, s1, sel);
-}
-__device__ __forceinline__ uint32_t xor3v(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-// Byte form of a row in a lane: 8 symbols as (lo dwords l0, l1; hi dwords h0, h1),
-// or in subfield coordinates (c0 dwords; c1 dwords).
-// A table's leading dwords held in SGPRs (loaded one row ahead of its use).
-template <int N>
-struct Tab {
-    uint32_t v[N];
-    __device__ __forceinline__ uint32_t operator[](int i) const { return v[i]; }
-};
-// Tab<N> of the table at p; p passes an empty volatile asm first, which fixes
-// where (in the sequence of volatile steps) the loads are issued.
-template <int N>
-__device__ __forceinline__ Tab<N> tab_at(cu32_t *p) {
-    asm volatile("" : "+s"(p));
-    Tab<N> t;
-#pragma unroll
-    for (int i = 0; i < N; i++) t.v[i] = p[i];
-    return t;
-}
-
-// x = y * table (full-field table, make_twiddle / make_linear_image layout).
-template <class T>
-__device__ __forceinline__ void mul16(uint32_t (&x)[4], const uint32_t (&y)[4], const T &t) {
-#pragma unroll
-    for (int d = 0; d < 2; d++) {
-        const uint32_t lo = y[d], hi = y[2 + d];
-        const uint32_t a0 = lo & 0x07070707u, a1 = (lo >> 3) & 0x07070707u, a2 = (lo >> 6) & 0x03030303u;
-        const uint32_t b0 = hi & 0x07070707u, b1 = (hi >> 3) & 0x07070707u, b2 = (hi >> 6) & 0x03030303u;
-        x[d] = xor3v(xor3v(perm(t[1], t[0], a0), perm(t[5], t[4], a1), perm(t[8], t[8], a2)), perm(t[11], t[10], b0),
-                     perm(t[15], t[14], b1)) ^ perm(t[18], t[18], b2);
-        x[2 + d] = xor3v(xor3v(perm(t[3], t[2], a0), perm(t[7], t[6], a1), perm(t[9], t[9], a2)), perm(t[13], t[12], b0),
-                         perm(t[17], t[16], b1)) ^ perm(t[19], t[19], b2);
-    }
-}
-// x ^= y * table (subfield table, make_sub_twiddle layout: the same byte map on c0 and c1;
-// a zero twiddle's table is all zero).
-template <class T>
-__device__ __forceinline__ void mul8_add(uint32_t *x, const uint32_t *y, const T &t) {
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-        const uint32_t v = y[d];
-        x[d] = xor3v(x[d] ^ perm(t[1], t[0], v & 0x07070707u), perm(t[3], t[2], (v >> 3) & 0x07070707u),
-                     perm(t[4], t[4], (v >> 6) & 0x03030303u));
-    }
-}
 
 // x ^= M * y over 8 planes (M row i: bit j set when plane j feeds plane i).
 template <int L, int G>
