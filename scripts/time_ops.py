@@ -32,6 +32,10 @@ CONFIGS = {
     "C3vx16": (16, 128, 32, 1 << 20, "verify", 16),
     # failing verify (every stripe corrupt): the flag path
     "C3vbadx16": (16, 128, 32, 1 << 20, "verify_bad", 16),
+    # the C5-geometry repair (n = 2048 work rows: the multi-pass reconstruct),
+    # 256 erasures, one stripe and one pattern over 8 stripes per launch
+    "C5r": (16, 1024, 256, 256 << 10, "reconstruct"),
+    "C5rb8": (16, 1024, 256, 256 << 10, "reconstruct", 8),
 }
 # Host-resident (PCIe-inclusive) variants: shards in host memory, rs_encode /
 # rs_reconstruct stream them through the GPU.  "p" = pinned rows (rs_host_alloc).
