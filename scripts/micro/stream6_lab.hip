@@ -89,6 +89,55 @@ __global__ void __launch_bounds__(256) k_tile_allfirst(uint8_t *base, uint32_t R
         __builtin_amdgcn_raw_buffer_store_b128(acc[j], rs, col, (uint32_t)(K + r0 + RPI * j) * RS, 0);
 }
 
+// 2 KB tiles whose 32 blocks come from NP pieces of 2048 / NP contiguous bytes
+// spread over the row (piece p at p * S / NP): concurrently running tiles then
+// cover consecutive narrow pieces, as narrow tiles do, while a workgroup
+// keeps k_encode_hp's 2 KB per row.  KL: the kernel's lane layout (lane =
+// 64-byte block, four 16-byte loads per row at 64-byte stride, rows r and
+// r + 4 in the two wave halves) instead of lane-contiguous loads.
+template <int NP, bool KL>
+__global__ void __launch_bounds__(256) k_tile_pieces(uint8_t *base, uint32_t RS, uint64_t SS) {
+    constexpr int PW = 2048 / NP;  // bytes per piece
+    const int tps = S / 2048;
+    const int stripe = blockIdx.x / tps, ct = blockIdx.x - stripe * tps;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)stripe * SS, 0, (int)((K + P) * RS), 0x00020000);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (!KL) {
+        // lane-contiguous: 128 lanes per row (2 KB), 2 rows per pass
+        const int c16 = t & 127;                  // 16-byte unit of the tile row
+        const int pc = (c16 * 16) / PW, within = (c16 * 16) % PW;
+        const uint32_t col = (uint32_t)pc * (S / NP) + (uint32_t)ct * PW + within;
+        const int r0 = t >> 7;
+#pragma unroll
+        for (int j = r0; j < P; j += 2) {
+            u32x4 a[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) a[q] = ldx<false>(rs, col, (uint32_t)(4 * j + q) * RS);
+            __builtin_amdgcn_raw_buffer_store_b128(a[0] ^ a[1] ^ a[2] ^ a[3], rs, col, (uint32_t)(K + j) * RS, 0);
+        }
+    } else {
+        // kernel layout: lane (b = lane & 31, h = lane >> 5) owns block b of rows
+        // 8w + 4h + i; each row is four 16-byte loads at 64-byte lane stride
+        const int b = lane & 31, h = lane >> 5;
+        const int pc = (b * 64) / PW, within = (b * 64) % PW;
+        const uint32_t col = (uint32_t)pc * (S / NP) + (uint32_t)ct * PW + within;
+#pragma unroll
+        for (int s = 0; s < 4; s++) {  // 4 steps of 32 input rows: 8 per wave, 4 per lane
+            u32x4 acc[4] = {};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t row = (uint32_t)(32 * s + 8 * w + 4 * h + i);
+#pragma unroll
+                for (int q = 0; q < 4; q++) acc[q] ^= ldx<false>(rs, col + 16 * q, row * RS);
+            }
+            // output row 8 s + 2 w + h (32 rows over the 4 steps)
+            const uint32_t orow = (uint32_t)(K + 8 * s + 2 * w + h);
+#pragma unroll
+            for (int q = 0; q < 4; q++) __builtin_amdgcn_raw_buffer_store_b128(acc[q], rs, col + 16 * q, orow * RS, 0);
+        }
+    }
+}
+
 // Plain 4:1 one-shot stream: block b reads U float4 per lane from each of 4
 // regions and writes their XOR to the destination.
 template <int U, bool NT>
@@ -159,6 +208,21 @@ int main(int argc, char **argv) {
         TILE(2048, 512, false, 0);
         TILE(512, 256, false, 1);
         TILE(512, 256, true, 1);
+        {
+            const unsigned g = (unsigned)((uint64_t)nst * (S / 2048));
+#define PIECES(NPC, KL)                                                                                          \
+    do {                                                                                                       \
+        snprintf(nm, sizeof nm, "C3 tile 2KB = %d x %dB pieces%s", NPC, 2048 / NPC, KL ? " kernel-layout" : ""); \
+        rep(nm, timeit([&] { hipLaunchKernelGGL((k_tile_pieces<NPC, KL>), dim3(g), dim3(256), 0, 0, slab, RS, SS); }), alg); \
+    } while (0)
+            PIECES(1, false);
+            PIECES(4, false);
+            PIECES(8, false);
+            PIECES(1, true);
+            PIECES(4, true);
+            PIECES(8, true);
+            PIECES(32, true);
+        }
         {
             const unsigned g = (unsigned)((uint64_t)nst * (S / 512));
             rep("C3 tile 512B all-loads-first", timeit([&] { hipLaunchKernelGGL((k_tile_allfirst<false>), dim3(g), dim3(256), 0, 0, slab, RS, SS); }), alg);
