@@ -94,6 +94,8 @@ struct DevPlan {
     const int *pos = nullptr;
     const int *src_idx = nullptr, *dst_idx = nullptr;  // pl.src_shard / pl.dst_shard (strided launches)
     uint32_t need[8] = {};
+    const uint32_t *need_w = nullptr;  // the revealed-row mask, n / 32 words (kernels read it for n > 256)
+    const int *rev = nullptr;          // output index of each work row, -1: not revealed (n > 256)
     // One event per stream that launched with this plan, recorded after each
     // such launch: an eviction frees blob only after the last launch on every
     // one of those streams (one event alone would cover only the latest).
@@ -448,6 +450,13 @@ int build_decode_plan(rs_codec *c) {
     int e = upload_twiddles(c, il, c->dtw_ifft);
     if (e) return e;
     return upload_twiddles(c, fl, c->dtw_fft);
+}
+
+// One LDS-resident reconstruct launch covers n <= 256 (both fields) and, for
+// GF(2^16), n up to 2048 (64-byte tiles, kernels.hpp kMaxLdsRecLogN16); larger
+// n runs the multi-pass kernels.
+bool rec_lds_ok(const rs_codec *c) {
+    return c->logn <= kMaxLdsLogN || (c->bits == 16 && c->logn <= kMaxLdsRecLogN16);
 }
 
 hipStream_t pick_stream(rs_codec *c, void *s) {
@@ -818,9 +827,20 @@ int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t s_in = pl.tw_in.size() * 4, s_out = pl.tw_out.size() * 4, s_pos = std::max<size_t>(pl.pos.size(), 1) * 4;
     const size_t s_si = pl.src_shard.size() * 4, s_di = std::max<size_t>(pl.dst_shard.size(), 1) * 4;
+    const size_t s_nw = (size_t)std::max(c->n / 32, 1) * 4, s_rev = (size_t)c->n * 4;
     const size_t o_out = al(s_in), o_pos = o_out + al(s_out), o_si = o_pos + al(s_pos), o_di = o_si + al(s_si);
-    const size_t total = o_di + al(s_di);
+    const size_t o_nw = o_di + al(s_di), o_rev = o_nw + al(s_nw);
+    const size_t total = o_rev + al(s_rev);
     std::vector<uint8_t> h(total, 0);
+    {
+        uint32_t *nw = (uint32_t *)(h.data() + o_nw);
+        int *rev = (int *)(h.data() + o_rev);
+        for (int r = 0; r < c->n; r++) rev[r] = -1;
+        for (size_t j = 0; j < pl.pos.size(); j++) {
+            nw[pl.pos[j] >> 5] |= 1u << (pl.pos[j] & 31);
+            rev[pl.pos[j]] = (int)j;
+        }
+    }
     std::memcpy(h.data(), pl.tw_in.data(), s_in);
     std::memcpy(h.data() + o_out, pl.tw_out.data(), s_out);
     if (!pl.pos.empty()) std::memcpy(h.data() + o_pos, pl.pos.data(), pl.pos.size() * 4);
@@ -833,14 +853,17 @@ int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
     dp->pos = (const int *)(dp->blob.p + o_pos);
     dp->src_idx = (const int *)(dp->blob.p + o_si);
     dp->dst_idx = (const int *)(dp->blob.p + o_di);
-    for (int p : pl.pos) dp->need[p >> 5] |= 1u << (p & 31);
+    dp->need_w = (const uint32_t *)(dp->blob.p + o_nw);
+    dp->rev = (const int *)(dp->blob.p + o_rev);
+    for (int p : pl.pos)
+        if (p < 256) dp->need[p >> 5] |= 1u << (p & 31);
     c->dplan_cache.emplace_front(std::move(key), std::move(dp));
     if (c->dplan_cache.size() > 16) c->dplan_cache.pop_back();  // waits for the plan's last launch
     *out = c->dplan_cache.front().second.get();
     return RS_OK;
 }
 
-// One launch of the n <= 256 reconstruct with a cached device plan over
+// One launch of the LDS-resident reconstruct (rec_lds_ok) with a cached device plan over
 // strided shards (shard i of stripe y at base + y * stripe_stride + i * stride).
 int launch_rec_plan(rs_codec *c, DevPlan *dpl, uint8_t *base, uint64_t stride, uint64_t stripe_stride, int nstripes,
                     uint64_t S, hipStream_t s) {
@@ -858,6 +881,8 @@ int launch_rec_plan(rs_codec *c, DevPlan *dpl, uint8_t *base, uint64_t stride, u
     ra.nd = nd;
     ra.prune = prune_enabled() ? 1 : 0;
     std::memcpy(ra.need, dpl->need, sizeof(ra.need));
+    ra.need_w = dpl->need_w;
+    ra.rev = dpl->rev;
     ra.base = base;
     ra.stride = stride;
     ra.stripe_stride = stripe_stride;
@@ -869,7 +894,7 @@ int launch_rec_plan(rs_codec *c, DevPlan *dpl, uint8_t *base, uint64_t stride, u
     return RS_OK;
 }
 
-// rs_reconstruct_dev with n <= 256 (one LDS-resident launch): the plan's tables
+// rs_reconstruct_dev with rec_lds_ok (one LDS-resident launch): the plan's tables
 // stay in HBM; equally strided shards (an AllocAligned slab, a torch 2-D
 // tensor) go to the kernel as base + stride, other layouts' row pointers
 // through a ring slot; nothing waits for the kernel -- the call is
@@ -893,6 +918,8 @@ int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uin
     ra.nd = nd;
     ra.prune = prune_enabled() ? 1 : 0;
     std::memcpy(ra.need, dp->need, sizeof(ra.need));
+    ra.need_w = dp->need_w;
+    ra.rev = dp->rev;
     {
         // strided: every shard the launch touches at d[0] + i * stride
         int i0 = -1, i1 = -1;
@@ -1127,13 +1154,13 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     const int k = c->k, total = c->total;
     std::vector<int> in_rows, out_rows;
     RecPlan pl;
-    // reconstruct with n <= 256: the pattern's tables stay in HBM (dev_plan)
+    // LDS-resident reconstruct (rec_lds_ok): the pattern's tables stay in HBM (dev_plan)
     // and every staging slab is strided (shard i at slab + i * seg), so the
     // call uploads nothing and never waits for the previous one
     DevPlan *dpl = nullptr;
     if (op == HostOp::Reconstruct) {
         if (int be = build_decode_plan(c)) return be;
-        if (c->dec_ok && c->logn <= kMaxLdsLogN) {
+        if (c->dec_ok && rec_lds_ok(c)) {
             e = dev_plan(c, present, recover_all, &dpl);
             if (e) return e;
             pl = dpl->pl;
@@ -1167,7 +1194,7 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     // reads; it waits only on ev_free[b].
     const uint64_t stage_cap = (uint64_t)c->stage.n / kHostBufs;  // >= slab_al
     // scratch of the multi-pass paths, sized before any launch (no realloc mid-pipeline)
-    // (the n <= 256 reconstruct plan and the m <= 256 LDS encode use none)
+    // (the LDS-resident reconstruct plan and the m <= 256 LDS encode use none)
     if (op == HostOp::Reconstruct && !dpl) e = scratch_ensure(c, c->work, (size_t)c->n * seg);
     else if (op != HostOp::Reconstruct && c->logm > kMaxLdsLogN) e = scratch_ensure(c, c->work, (size_t)2 * c->m * seg);
     if (e) return e;
@@ -1598,7 +1625,7 @@ int rs_reconstruct_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size
     if (int ie = ensure_device(c)) return ie;
     const hipStream_t s = pick_stream(c, stream);
     if (int e = build_decode_plan(c)) return e;
-    if (c->dec_ok && c->logn <= kMaxLdsLogN) {
+    if (c->dec_ok && rec_lds_ok(c)) {
         // one launch: grid.y = stripe, the pattern's tables shared (dev_plan cache)
         DevPlan *dpl = nullptr;
         if (int e = dev_plan(c, pr, recover_all != 0, &dpl)) return e;
@@ -1637,7 +1664,7 @@ int rs_reconstruct_dev(rs_codec *c, uint8_t *const *d, const uint8_t *present, s
     if (int ie = ensure_device(c)) return ie;
     const hipStream_t s = pick_stream(c, stream);
     if (int e = build_decode_plan(c)) return e;
-    if (c->dec_ok && c->logn <= kMaxLdsLogN) {
+    if (c->dec_ok && rec_lds_ok(c)) {
         if (int e = reconstruct_device_lds(c, d, pr, S, recover_all != 0, s)) return e;
         if (!stream) HIP_TRY(hipStreamSynchronize(s));  // no caller stream: complete on return
         return RS_OK;

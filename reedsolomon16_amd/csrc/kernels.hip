@@ -1261,14 +1261,23 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
             return v;
         }
     };
+    // n > 256: the revealed-row mask and the output indices come from HBM
+    constexpr bool BIG = LOGN > 8;
+    typedef typename std::conditional<BIG, NeedMem, Need>::type NeedT;
+    auto need_of = [&]() {
+        if constexpr (BIG) return NeedMem{(const __attribute__((address_space(4))) uint32_t *)a.need_w};
+        else return load_need(a.need);
+    };
     // reveal: shard = work[pos] * (modulus - errLocs[pos])
     struct Reveal {
         const RecArgs &a;
         uint64_t tile;
         uint8_t *sbase;
-        Need nw;
+        NeedT nw;
         __device__ void operator()(int r, int u, const V &x) const {
-            const int j = reveal_index(nw, a.m, r);  // output index from the revealed-row mask
+            int j;  // output index of work row r (-1: not revealed)
+            if constexpr (BIG) j = a.rev[r];
+            else j = reveal_index(nw, a.m, r);  // from the revealed-row mask
             if (j < 0 || !L::valid(tile, a.S, u)) return;
             V v = F::zero();
             F::mul_add(v, x, a.tw_out + (uint64_t)j * F::TWD);
@@ -1278,7 +1287,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
     };
     const LdsIO<FT> lio{lds};
     lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
-    const Reveal rv{a, tile, sbase, load_need(a.need)};
+    const Reveal rv{a, tile, sbase, need_of()};
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
     if constexpr (LOGN >= 3) {
         // fused with the FFT's first pass (radix-4 at dist D = N/4, one group,
@@ -1319,7 +1328,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         }
         __syncthreads();
         if (a.prune) {
-            lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, Need, 1>(lds, a.mtrunc, a.tw_fft, load_need(a.need), lio, rv);
+            lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NeedT, 1>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
         } else {
             lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NoNeed, 1>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
         }
@@ -1349,7 +1358,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         __syncthreads();
     }
     if (a.prune) {
-        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, load_need(a.need), lio, rv);
+        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
     } else {
         lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
     }
@@ -1510,6 +1519,15 @@ hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
         case 6: return rec_lds_t<F, FT, 6>(a, s);
         case 7: return rec_lds_t<F, FT, 7>(a, s);
         case 8: return rec_lds_t<F, FT, 8>(a, s);
+    }
+    // n = 512 .. 2048: GF(2^16) in full-field coordinates, 64-byte tiles (the
+    // n x 80-byte image fills the 160 KB LDS at n = 2048)
+    if constexpr (std::is_same<F, F16<2>>::value && std::is_same<FT, F>::value) {
+        switch (logn) {
+            case 9: return rec_lds_t<F, FT, 9>(a, s);
+            case 10: return rec_lds_t<F, FT, 10>(a, s);
+            case 11: return rec_lds_t<F, FT, 11>(a, s);
+        }
     }
     return hipErrorInvalidValue;
 }
@@ -1708,6 +1726,10 @@ hipError_t rec_lds_w(int bits, int logn, bool sub, const RecArgs &a, hipStream_t
 }
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s) {
     if (rec_bs256_available(bits, logn, sub, a.mtrunc)) return launch_rec_bs256(a, s);
+    if (logn > 8) {
+        if (bits != 16 || sub || logn > kMaxLdsRecLogN16 || !a.need_w || !a.rev) return hipErrorInvalidValue;
+        return rec_lds_f<F16<2>>(logn, a, s);
+    }
     const uint64_t ns = a.base && a.nstripes > 1 ? (uint64_t)a.nstripes : 1;
     const bool narrow = pick_narrow((a.S + 127) / 128 * ns < kLdsMinGrid);
     return narrow ? rec_lds_w<2>(bits, logn, sub, a, s) : rec_lds_w<4>(bits, logn, sub, a, s);

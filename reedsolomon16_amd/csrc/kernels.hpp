@@ -74,7 +74,7 @@ hipError_t launch_reveal(int bits, uint8_t *const *dst, const uint8_t *work, uin
 
 
 // ---- LDS-resident paths: one workgroup per 128-byte tile of every row ----
-// Reconstruct of one stripe over n = 2^logn <= 256 work rows.
+// Reconstruct of one stripe over n = 2^logn <= 2048 work rows.
 struct RecArgs {
     const uint8_t *const *src;  // n device row pointers (nullptr: zero row)
     uint8_t *const *dst;        // nd output rows
@@ -100,9 +100,15 @@ struct RecArgs {
     // is revealed; FFT groups whose rows are all unset are skipped.
     int prune;
     uint32_t need[8];           // n <= 256 rows
+    // n = 512 .. 2048 (GF(2^16), 64-byte tiles): the revealed-row mask as n / 32
+    // words and each work row's output index (-1: not revealed), both in HBM
+    const uint32_t *need_w;
+    const int *rev;
 };
 // sub: GF(2^16) transforms in subfield coordinates (tw_ifft/tw_fft are
 // kTwDwords8 subfield tables; tw_in/tw_out fold in the coordinate change).
+// logn <= 8, or GF(2^16) with logn <= kMaxLdsRecLogN16 (full field, need_w / rev set).
+constexpr int kMaxLdsRecLogN16 = 11;
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s);
 // Bit-sliced reconstruct (csrc/bitslice_dec.hip): GF(2^16), n = 256, transforms
 // in subfield coordinates (tw_ifft / tw_fft: kTwDwords8 subfield tables,

@@ -37,6 +37,19 @@ __device__ __forceinline__ bool rows_needed(const Need &n, int lo, int cnt) {
     return ((word >> (lo & 31)) & ((1u << cnt) - 1)) != 0;
 }
 __device__ __forceinline__ bool rows_needed(const NoNeed &, int, int) { return true; }
+// n > 256: the mask's words in HBM (constant address space: wave-uniform
+// indices become scalar loads)
+struct NeedMem {
+    const __attribute__((address_space(4))) uint32_t *w;
+};
+__device__ __forceinline__ bool rows_needed(const NeedMem &n, int lo, int cnt) {
+    if (cnt >= 32) {
+        uint32_t acc = 0;
+        for (int k = lo >> 5; k < (lo + cnt) >> 5; k++) acc |= n.w[k];
+        return acc != 0;
+    }
+    return ((((const uint32_t *)n.w)[lo >> 5] >> (lo & 31)) & ((1u << cnt) - 1)) != 0;
+}
 __device__ __forceinline__ Need load_need(const uint32_t (&src)[8]) {
     Need n;
 #pragma unroll
