@@ -1115,7 +1115,7 @@ __device__ __forceinline__ void lds_sync() { __syncthreads(); }
 // need (forward passes only): skip groups none of whose rows is read later --
 // the pruning of errorBitfield.fftDIT (leopard16.go:1215-1252); the rows that
 // are read come out identical.
-template <class F, bool INV, class In, class Out, class NeedT>
+template <class F, bool INV, class In, class Out, class NeedT, int NT = 256>
 __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active, const uint32_t *__restrict__ tw,
                                          NeedT need, const In &in, const Out &out) {
     typedef LTile<F> L;
@@ -1143,16 +1143,16 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
             // A wave's 64 items (aligned) lie in one group: the group index is
             // wave-uniform, so its twiddle tables come in by scalar loads and
             // the zero-twiddle test is a scalar branch.
-            for (int it = threadIdx.x; it < items; it += 256)
+            for (int it = threadIdx.x; it < items; it += NT)
                 group(it, __builtin_amdgcn_readfirstlane((it / U) >> ld), std::false_type{});
         } else
         {
-            for (int it = threadIdx.x; it < items; it += 256) group(it, (it / U) >> ld, std::bool_constant<kLdsBranchFree>{});
+            for (int it = threadIdx.x; it < items; it += NT) group(it, (it / U) >> ld, std::bool_constant<kLdsBranchFree>{});
         }
     } else {
         // inverse: pairs (j, j + dist), j < dist, one twiddle; forward: dist 1, pairs (2g, 2g+1), twiddle g
         const int pairs = INV ? dist : groups_active;
-        for (int it = threadIdx.x; it < pairs * U; it += 256) {
+        for (int it = threadIdx.x; it < pairs * U; it += NT) {
             const int q = it / U, u = it - q * U;
             const int rx = INV ? q : 2 * q, ry = INV ? q + dist : 2 * q + 1;
             if (!INV && !rows_needed(need, 2 * q, 2)) continue;
@@ -1172,7 +1172,7 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
 // first pass reads through `in`, the last writes through `out`.  A first pass
 // that does not read the LDS image runs every group (rows past mtrunc come in
 // as zero, and zero rows transform to zero rows): later passes read those rows.
-template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed, int P0 = 0, int P1 = 32>
+template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed, int P0 = 0, int P1 = 32, int NT = 256>
 __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
                                               NeedT need, const In &in, const Out &out) {
     constexpr int N = 1 << LOGN, NP4 = LOGN / 2, NP = NP4 + (LOGN & 1);
@@ -1199,7 +1199,7 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
                 // groups past mtrunc hold zero rows: zero their LDS rows instead
                 // of transforming them (the pass's barrier covers these stores)
                 const int z0 = active * 4 * dist;
-                for (int it = threadIdx.x; it < (N - z0) * LTile<F>::U; it += 256)
+                for (int it = threadIdx.x; it < (N - z0) * LTile<F>::U; it += NT)
                     lio(z0 + it / LTile<F>::U, it % LTile<F>::U, F::zero());
             } else if constexpr (from_hbm) {
                 active = groups;
@@ -1209,8 +1209,8 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
         }
         const uint32_t *t = tw + (uint64_t)slot * F::TWD;
         auto run = [=](const auto &pin, const auto &pout) {
-            if constexpr (INV) lds_pass<F, INV>(dist, radix4 ? 4 : 2, active, t, NoNeed{}, pin, pout);
-            else lds_pass<F, INV>(dist, radix4 ? 4 : 2, active, t, need, pin, pout);
+            if constexpr (INV) lds_pass<F, INV, std::decay_t<decltype(pin)>, std::decay_t<decltype(pout)>, NoNeed, NT>(dist, radix4 ? 4 : 2, active, t, NoNeed{}, pin, pout);
+            else lds_pass<F, INV, std::decay_t<decltype(pin)>, std::decay_t<decltype(pout)>, NeedT, NT>(dist, radix4 ? 4 : 2, active, t, need, pin, pout);
         };
         if constexpr (from_hbm) {
             if constexpr (p == NP - 1) run(in, out);
@@ -1234,12 +1234,16 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
 // F16S when every transform twiddle lies in GF(2^8)).  The scale-in feeds the
 // IFFT's first pass straight from HBM and the FFT's last pass reveals straight
 // to the output rows.
+// Threads per workgroup: 256, and 1024 for n >= 1024 (the n x 64-byte image
+// leaves room for one or two workgroups per CU: 16 waves keep the SIMDs fed).
+template <int LOGN> constexpr int rec_lds_threads() { return LOGN >= 10 ? 1024 : 256; }
+
 template <class F, class FT, int LOGN>
-__global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
+__global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
-    constexpr int N = 1 << LOGN, U = L::U;
-    constexpr int K = (N * U + 255) / 256;  // derivative outputs per thread
+    constexpr int N = 1 << LOGN, U = L::U, NT = rec_lds_threads<LOGN>();
+    constexpr int K = (N * U + NT - 1) / NT;  // derivative outputs per thread
     __shared__ __attribute__((aligned(16))) uint8_t lds[N * L::ROW];
     const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
     uint8_t *const sbase = a.base ? a.base + (uint64_t)blockIdx.y * a.stripe_stride : nullptr;  // this stripe
@@ -1286,7 +1290,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         }
     };
     const LdsIO<FT> lio{lds};
-    lds_transform<FT, true, LOGN>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
+    lds_transform<FT, true, LOGN, ScaleIn, LdsIO<FT>, NoNeed, 0, 32, NT>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
     const Reveal rv{a, tile, sbase, need_of()};
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
     if constexpr (LOGN >= 3) {
@@ -1295,11 +1299,11 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         // i + aD from the IFFT image (the a-bit terms from the rows it holds),
         // transforms them, and stores them after every thread has read.
         constexpr int D = N / 4;
-        constexpr int KF = (D * U + 255) / 256;  // fused items per thread
+        constexpr int KF = (D * U + NT - 1) / NT;  // fused items per thread
         V x[KF][4];
 #pragma unroll
         for (int k = 0; k < KF; k++) {
-            const int it = threadIdx.x + 256 * k;
+            const int it = threadIdx.x + NT * k;
             if (it < D * U) {
                 const int i = it / U, u = it - i * U;
                 V X[4];
@@ -1319,7 +1323,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < KF; k++) {
-            const int it = threadIdx.x + 256 * k;
+            const int it = threadIdx.x + NT * k;
             if (it < D * U) {
                 const int i = it / U, u = it - i * U;
 #pragma unroll
@@ -1328,9 +1332,9 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         }
         __syncthreads();
         if (a.prune) {
-            lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NeedT, 1>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
+            lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NeedT, 1, 32, NT>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
         } else {
-            lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NoNeed, 1>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
+            lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NoNeed, 1, 32, NT>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
         }
         return;
     }
@@ -1338,7 +1342,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         V o[K];
 #pragma unroll
         for (int k = 0; k < K; k++) {
-            const int it = threadIdx.x + 256 * k;
+            const int it = threadIdx.x + NT * k;
             if (it < N * U) {
                 const int r = it / U, u = it - r * U;
                 o[k] = L::get(lds, r, u);
@@ -1349,7 +1353,7 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < K; k++) {
-            const int it = threadIdx.x + 256 * k;
+            const int it = threadIdx.x + NT * k;
             if (it < N * U) {
                 const int r = it / U, u = it - r * U;
                 L::put(lds, r, u, o[k]);
@@ -1358,9 +1362,9 @@ __global__ void __launch_bounds__(256) k_rec_lds(RecArgs a) {
         __syncthreads();
     }
     if (a.prune) {
-        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
+        lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NeedT, 0, 32, NT>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
     } else {
-        lds_transform<FT, false, LOGN>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
+        lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NoNeed, 0, 32, NT>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
     }
 }
 
@@ -1499,13 +1503,13 @@ template <class F, class FT, int LOGN>
 hipError_t rec_lds_t(const RecArgs &a, hipStream_t s) {
     const unsigned gx = (unsigned)((a.S + LTile<F>::TB - 1) / LTile<F>::TB);
     if (!a.base || a.nstripes <= 1) {
-        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), dim3(gx), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), dim3(gx), dim3(rec_lds_threads<LOGN>()), 0, s, a);
         return hipGetLastError();
     }
     return for_y(a.nstripes, [&](int y0, int ny) {  // batched strided stripes: grid.y = stripe
         RecArgs b = a;
         b.base = a.base + (uint64_t)y0 * a.stripe_stride;
-        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), dim3(gx, (unsigned)ny), dim3(256), 0, s, b);
+        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), dim3(gx, (unsigned)ny), dim3(rec_lds_threads<LOGN>()), 0, s, b);
     });
 }
 template <class F, class FT = F>
