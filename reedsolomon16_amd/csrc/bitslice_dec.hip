@@ -128,7 +128,8 @@ constexpr uint32_t z_after(uint32_t z, int qb) {
 typedef __attribute__((address_space(4))) const RecArgs cargs_t;
 
 // RS_DEC_ABL: bitmask of steps left out (build experiments only; wrong results):
-// 1 row loads, 2 phase-1 transform, 4 phase 2, 8 phase-3 transform, 16 reveal
+// 1 row loads, 2 phase-1 transform, 4 phase 2, 8 phase-3 transform, 16 reveal,
+// 32 scale-in, 64 phase-1 / phase-3 byte <-> plane transposes
 #ifndef RS_DEC_ABL
 #define RS_DEC_ABL 0
 #endif
@@ -394,10 +395,10 @@ struct Dec {
             return;
         }
         if constexpr (!ABL(0)) load_rows(u);
-        scale(u);
+        if constexpr (!ABL(5)) scale(u);
         if constexpr (!ABL(1)) ifft0_bytes(u);
         for (int b = 0; b < nbar; b++) lds_barrier();
-        to_planes(0xFFu);
+        if constexpr (!ABL(6)) to_planes(0xFFu);
         if constexpr (!ABL(1)) ifft_a(u);
     }
     // V[0..7] <-> V[8..15] (the parked unit)
@@ -538,7 +539,7 @@ struct Dec {
         uint32_t pairs = 0;  // register rows holding a revealed row (either z)
 #pragma unroll
         for (int i = 0; i < 8; i++) pairs |= ((nw >> (2 * i)) & 3u) ? 1u << i : 0u;
-        to_bytes(pairs);
+        if constexpr (!ABL(6)) to_bytes(pairs);
         fft0_bytes(u, nw);
         if constexpr (!ABL(4)) reveal(u, nw, need);
     }
@@ -563,18 +564,35 @@ struct Dec {
         }
         if (u & 1) below += __builtin_popcount(word & 0xFFFFu);
         const int j_hi = below - below_m, j_lo = total - below_m + below;
+        auto jof = [&](int t) {  // output index of row 16 u + t (wave-uniform, scalar)
+            return (16 * u + t >= a.m ? j_hi : j_lo) + __builtin_popcount(nw & ((1u << t) - 1u));
+        };
         const uint32_t off = lane_off();
+        // The next revealed row's table and output row are loaded while this
+        // one is multiplied and stored (scalar loads issued at use left every
+        // revealed row waiting on two dependent loads).
+        const int j0 = jof(__builtin_ctz(nw));
+        Tab<20> cur = tab_at<20>(ctab(a.tw_out) + (uint64_t)j0 * kTw16);
+        uint8_t *row = dst_row(a, j0);
         sfor<16>([&](auto T) __attribute__((always_inline)) {
             constexpr int t = decltype(T)::value;
             if ((nw >> t) & 1u) {
-                const int r = 16 * u + t;
-                const int j = (r >= a.m ? j_hi : j_lo) + __builtin_popcount(nw & ((1u << t) - 1u));
+                const uint32_t rest = nw & ~((2u << t) - 1u);
+                Tab<20> nxt = cur;
+                uint8_t *nrow = row;
+                if (rest) {
+                    const int jn = jof(__builtin_ctz(rest));
+                    nxt = tab_at<20>(ctab(a.tw_out) + (uint64_t)jn * kTw16);
+                    nrow = dst_row(a, jn);
+                }
                 uint32_t o[4];
                 uint32_t y[4] = {bytes(t)[0], bytes(t)[1], bytes(t)[2], bytes(t)[3]};
-                mul16(o, y, tab_at<20>(ctab(a.tw_out) + (uint64_t)j * kTw16));
+                mul16(o, y, cur);
                 swap32(o[0], o[2]);  // back to lo bytes (p = 0) / hi bytes (p = 1) of symbols 16g..16g+15
                 swap32(o[1], o[3]);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{o[0], o[1], o[2], o[3]}, row_rsrc(a, dst_row(a, j)), off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{o[0], o[1], o[2], o[3]}, row_rsrc(a, row), off, 0, 0);
+                cur = nxt;
+                row = nrow;
             }
             __builtin_amdgcn_sched_barrier(0);
         });

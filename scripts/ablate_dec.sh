@@ -9,7 +9,7 @@ HIPCC=/opt/rocm/bin/hipcc
 SRC=reedsolomon16_amd/csrc
 B=reedsolomon16_amd/build
 rm -rf build/ablate_dec; mkdir -p build/ablate_dec
-VARS=${VARIANTS:-"base:0 load:1 p1:2 phase2:4 p3:8 reveal:16"}
+VARS=${VARIANTS:-"base:0 load:1 p1:2 phase2:4 p3:8 reveal:16 scale:32 transp:64"}
 for v in $VARS; do
   IFS=: read -r name abl flags <<< "$v"
   mkdir -p build/ablate_dec/$name
@@ -18,5 +18,5 @@ done
 wait
 for v in $VARS; do
   name=${v%%:*}; d=build/ablate_dec/$name
-  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $d/librs_mi355x.so $B/kernels.o $B/bitslice.o $d/bitslice_dec.o $B/gf_host.o $B/codec.o
+  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $d/librs_mi355x.so $B/kernels.o $B/bitslice.o $d/bitslice_dec.o $B/bitslice_enc256.o $B/gf_host.o $B/codec.o
 done
