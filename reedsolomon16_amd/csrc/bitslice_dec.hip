@@ -564,9 +564,14 @@ struct Dec {
         }
         if (u & 1) below += __builtin_popcount(word & 0xFFFFu);
         const int j_hi = below - below_m, j_lo = total - below_m + below;
-        auto jof = [&](int t) {  // output index of row 16 u + t (wave-uniform, scalar)
-            return (16 * u + t >= a.m ? j_hi : j_lo) + __builtin_popcount(nw & ((1u << t) - 1u));
-        };
+        const uint32_t off = lane_off();
+        sfor<16>([&](auto T) __attribute__((always_inline)) {
+            constexpr int t = decltype(T)::value;
+            if ((nw >> t) & 1u) {
+                const int r = 16 * u + t;
+                const int j = (r >= a.m ? j_hi : j_lo) + __builtin_popcount(nw & ((1u << t) - 1u));
+                uint32_t o[4];
+                uint32_t y[4] = {bytes(t)[0], bytes(t)[1], bytes(t)[2], bytes(t)[3]};
         const uint32_t off = lane_off();
         // The next revealed row's table and output row are loaded while this
         // one is multiplied and stored (scalar loads issued at use left every
