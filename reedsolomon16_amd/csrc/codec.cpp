@@ -145,8 +145,6 @@ struct rs_codec {
     DevBuf<uint32_t> tw_ifft, tw_fft;
     bool split_ok = false;            // half-wave split kernel available (GF(2^16), 4 <= m <= 32)
     bool bs_ok = false;               // bit-sliced kernel covers (k, p) (GF(2^16), m = 16 or 32)
-    bool bs256_ok = false;            // bit-sliced m = 256 kernel covers (k, p) (bitslice_enc256.hip)
-    DevBuf<uint32_t> tw_bf, tw_bf_fft;  // its byte-form layer tables (E256Args)
     int cus = 0;                      // compute units of the device (persistent grids)
     DevBuf<uint32_t> tws_ifft, tws_fft;
     // LDS-kernel encode (GF(2^16), even log m): the final FFT's subfield tables
@@ -229,7 +227,7 @@ struct rs_codec {
             (void)hipEventSynchronize(scratch_ev);
             (void)hipEventDestroy(scratch_ev);
         }
-        tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); tw_fft_sub.release(); tw_dmap.release(); tw_bf.release(); tw_bf_fft.release(); dtw_ifft.release(); dtw_fft.release();
+        tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); tw_fft_sub.release(); tw_dmap.release(); dtw_ifft.release(); dtw_fft.release();
         work.release(); rows.release();
         if (hflag) (void)hipHostFree(hflag);
         if (dflag) (void)hipFree(dflag);
@@ -344,44 +342,6 @@ void plan_encode_host(rs_codec *c) {
     c->bs_ok = c->enc_ok && c->bits == 16 && (c->logm == 4 || c->logm == 5) && bs_enabled() &&
                encode_bs_available(c->k, c->p, c->enc_ifft_logs.data(), c->enc_fft_logs.data(), c->F->mod);
     if (c->bs_ok) c->path = std::string("bs16-m") + std::to_string(c->m);
-    c->bs256_ok = c->enc_ok && c->bits == 16 && c->logm == 8 && bs_enabled() && sub_coords().ok &&
-                  encode_bs256_available(c->k, c->p, c->enc_ifft_logs.data(), c->enc_fft_logs.data(), c->F->mod);
-    if (c->bs256_ok) c->path = "bs16-m256";
-}
-
-// Byte-form layer tables of the m = 256 bit-sliced encode (kernels.hpp
-// E256Args): chunk c's IFFT layers 0-2 use fftSkew[(c+1)256 - 1 + g 2^(L+1) + 2^L]
-// (ifftDITEncoder leopard16.go:699-741), the FFT's layers 1 and 0 fftSkew[g 2^(L+1) + 2^L - 1]
-// (fftDIT :618-657).  Each is checked against the geometry's own schedule
-// (entries == mod are groups the reference skips: their rows are zero).
-int upload_bs256(rs_codec *c) {
-    const Field &F = *c->F;
-    const int is = ifft_slots(8);
-    std::vector<uint32_t> bf((size_t)c->nchunks * 224 * kTwDwords16, 0), bff((size_t)192 * kTwDwords8, 0), dm(kTwDwords8, 0);
-    static const int off[3] = {0, 128, 192};
-    for (int ch = 0; ch < c->nchunks; ch++)
-        for (int L = 0; L < 3; L++)
-            for (int g = 0; g < (128 >> L); g++) {
-                const uint32_t lg = F.skew[(size_t)(ch + 1) * 256 - 1 + (size_t)g * (2u << L) + (1u << L)];
-                const uint32_t sl = c->enc_ifft_logs[(size_t)ch * is + ifft_slot(8, L, g * (2 << L))];
-                if (sl != F.mod && sl != lg) return RS_ERR_DEVICE;  // cannot happen: same formula
-                make_twiddle(F, lg, bf.data() + ((size_t)ch * 224 + off[L] + g) * kTwDwords16, true);
-            }
-    for (int L = 0; L < 2; L++)
-        for (int g = 0; g < (128 >> L); g++) {
-            const uint32_t lg = F.skew[(size_t)g * (2u << L) + (1u << L) - 1];
-            const uint32_t sl = c->enc_fft_logs[fft_slot(8, L, g * (2 << L))];
-            if ((sl != F.mod && sl != lg) || !in_subfield(F, lg)) return RS_ERR_DEVICE;
-            make_sub_twiddle(F, lg, bff.data() + ((L == 0 ? 0 : 128) + g) * kTwDwords8);
-        }
-    make_sub_dmap(dm.data());
-    HIP_TRY(c->tw_bf.ensure(bf.size()));
-    HIP_TRY(c->tw_bf_fft.ensure(bff.size()));
-    HIP_TRY(c->tw_dmap.ensure(dm.size()));
-    HIP_TRY(hipMemcpy(c->tw_bf.p, bf.data(), bf.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(c->tw_bf_fft.p, bff.data(), bff.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(c->tw_dmap.p, dm.data(), dm.size() * 4, hipMemcpyHostToDevice));
-    return RS_OK;
 }
 
 // Device half, on first use: stream, flag word, encode twiddle tables.
@@ -414,10 +374,6 @@ int ensure_device(rs_codec *c) {
             HIP_TRY(hipMemcpy(c->tw_fft_sub.p, hf.data(), hf.size() * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(c->tw_dmap.p, dm.data(), dm.size() * 4, hipMemcpyHostToDevice));
             c->fft_sub = true;
-        }
-        if (c->bs256_ok) {
-            e = upload_bs256(c);
-            if (e) return e;
         }
     }
     c->dev_ready = true;
@@ -602,26 +558,6 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
             return RS_OK;
         }
         HIP_TRY(launch_encode_reg(c->bits, c->logm, mismatch != nullptr, a, s));
-        return RS_OK;
-    }
-    if (c->bs256_ok && !data.table && !par.table && data.stride == par.stride && data.stride >= S &&
-        encode_bs256_fits(c->k, data.stride, S)) {  // bit-sliced m = 256
-        E256Args b{};
-        b.data = data.base;
-        b.parity = par.base;
-        b.row_stride = data.stride;
-        b.stripe_stride = stripe_stride;
-        b.S = S;
-        b.k = c->k;
-        b.p = c->p;
-        b.nstripes = nstripes;
-        b.nch = c->nchunks;
-        b.tw_bf = c->tw_bf.p;
-        b.tw_bf_fft = c->tw_bf_fft.p;
-        b.dmap = c->tw_dmap.p;
-        b.mismatch = mismatch;
-        if (!c->cus) HIP_TRY(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
-        HIP_TRY(launch_encode_bs256(mismatch != nullptr, b, c->cus, s));
         return RS_OK;
     }
     if (c->logm <= kMaxLdsLogN) {  // m rows of accumulator + chunk LDS-resident

@@ -1245,7 +1245,14 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
     constexpr int N = 1 << LOGN, U = L::U, NT = rec_lds_threads<LOGN>();
     constexpr int K = (N * U + NT - 1) / NT;  // derivative outputs per thread
     __shared__ __attribute__((aligned(16))) uint8_t lds[N * L::ROW];
-    const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
+    uint32_t bx = blockIdx.x;
+    if constexpr (LOGN > 8) {
+        // 64-byte tiles: the two tiles of a 128-byte line go to one XCD
+        // (workgroups are dealt round-robin over the 8 XCDs, each with its own
+        // L2): blocks 16q + x and 16q + x + 8 take tiles 16q + 2x, 16q + 2x + 1
+        if (bx < (gridDim.x & ~15u)) bx = (bx & ~15u) | ((bx & 7u) << 1) | ((bx >> 3) & 1u);
+    }
+    const uint64_t tile = (uint64_t)bx * L::TB;
     uint8_t *const sbase = a.base ? a.base + (uint64_t)blockIdx.y * a.stripe_stride : nullptr;  // this stripe
     // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0
     struct ScaleIn {

@@ -146,26 +146,4 @@ bool encode_bs_fits(int k, int p, uint64_t row_stride, uint64_t S);
 hipError_t launch_encode_bs(bool verify, const BsArgs &a, int cus, hipStream_t s);
 
 
-// ---- Bit-sliced encode for m = 256 (csrc/bitslice_enc256.hip): GF(2^16),
-// 129 <= p <= 256, k <= 1024 (four chunks).  Strided rows, one row stride for
-// data and parity.  The byte-form layers' tables come from the host:
-// tw_bf = nch x 224 full-field images (make_twiddle, kTwDwords16) of chunk c's
-// IFFT layer 0 (groups 0..127), 1 (128..191) and 2 (192..223); tw_bf_fft = the
-// FFT's subfield images (make_sub_twiddle, kTwDwords8) of layer 0 (0..127) and
-// layer 1 (128..191); dmap = make_sub_dmap.
-struct E256Args {
-    const uint8_t *data;
-    uint8_t *parity;
-    uint64_t row_stride, stripe_stride, S;
-    int k, p, nstripes, nch;
-    int tiles_per_stripe, ntiles;  // set by the launcher
-    uint32_t span, pspan;          // set by the launcher
-    const uint32_t *tw_bf, *tw_bf_fft, *dmap;
-    int *mismatch;
-};
-// True when the compiled networks agree with the geometry's own schedule.
-bool encode_bs256_available(int k, int p, const uint32_t *ifft_logs, const uint32_t *fft_logs, uint32_t mod);
-bool encode_bs256_fits(int k, uint64_t row_stride, uint64_t S);
-hipError_t launch_encode_bs256(bool verify, E256Args a, int cus, hipStream_t s);
-
 }  // namespace rs

@@ -206,6 +206,19 @@ int main(int argc, char **argv) {
         TILE(2048, 256, false, 0);
         TILE(2048, 256, true, 0);
         TILE(2048, 512, false, 0);
+        // occupancy held to the engine's (2 x 4 waves per CU at 64 KB LDS) by
+        // dynamic LDS that the kernel never touches
+#define TILEO(TW, BS, LDSKB)                                                                                        \
+    do {                                                                                                            \
+        const unsigned g = (unsigned)((uint64_t)nst * (S / TW));                                                    \
+        snprintf(nm, sizeof nm, "C3 tile %dB bs%d, %d KB LDS per WG", TW, BS, LDSKB);                             \
+        rep(nm, timeit([&] { hipLaunchKernelGGL((k_tile<TW, BS, false, 0>), dim3(g), dim3(BS), LDSKB << 10, 0, slab, RS, SS, nst); }), alg); \
+    } while (0)
+        TILEO(2048, 256, 64);
+        TILEO(512, 64, 20);
+        TILEO(512, 64, 40);
+        TILEO(512, 128, 40);
+        TILEO(512, 256, 64);
         TILE(512, 256, false, 1);
         TILE(512, 256, true, 1);
         {

@@ -328,113 +328,3 @@ def test_decode_split_equals_reference_chain(mtrunc):
         _layer(F, h, L, False)
     assert np.array_equal(h[:mtrunc], ref[:mtrunc])
 
-
-# ---------------------------------------------------------------- bit-sliced m = 256 encode (bitslice_enc256.hip)
-def load_enctab256():
-    if not os.path.exists(HDR):
-        pytest.skip("build/bs_tables.h not generated (run __graft_entry__.build())")
-    body = re.search(r"struct EncTab256 \{(.*?)\n\};", open(HDR).read(), re.S).group(1)
-
-    def arr(name):
-        blk = re.search(r"\b" + name + r"\[[^=]*= *(\{.*?\});", body, re.S).group(1)
-        return np.array([int(x) for x in re.findall(r"\d+", blk)], np.int64)
-
-    nch = int(re.search(r"NCH = (\d+)", body).group(1))
-    return nch, arr("m8").reshape(nch, 8, 128, 8), arr("logs").reshape(nch, 8, 128)
-
-
-def _bf_layers(c):
-    """Chunk c's layers that k_enc_bs256 runs in byte form (full-field twiddles)."""
-    return (0, 1, 2) if c == 3 else (0, 1)
-
-
-def test_enctab256_logs_and_subfield_split():
-    """EncTab256: chunk c, layer L, group g holds fftSkew[(c+1) 256 - 1 + g 2^(L+1) + 2^L]
-    (ifftDITEncoder's skewLUT[iend], leopard16.go:699-741), its 8x8 matrix in
-    subfield coordinates wherever the kernel runs the layer as a network, and
-    every such twiddle lies in the subfield, so the byte-form layers (0, 1, and
-    2 for c = 3) hold every full-field twiddle (chunk 0's layer 1 is subfield
-    too but runs in byte form with the others)."""
-    from oracle import leopard_np as lnp
-
-    F = lnp.field(16)
-    nch, m8, logs = load_enctab256()
-    assert nch == 4
-    for c in range(nch):
-        for L in range(8):
-            for g in range(128):
-                if g >= 128 >> L:
-                    assert logs[c, L, g] == F.mod
-                    continue
-                lg = int(F._skew[(c + 1) * 256 - 1 + g * (2 << L) + (1 << L)])
-                assert logs[c, L, g] == lg, (c, L, g)
-                cols = [int(F.mul_log(1 << j, lg)) if lg != F.mod else 0 for j in range(8)]
-                sub = all(x < 256 for x in cols)
-                if L in _bf_layers(c):
-                    continue
-                assert sub, (c, L, g)
-                for j in range(8):
-                    for i in range(8):
-                        assert ((m8[c, L, g, i] >> j) & 1) == ((cols[j] >> i) & 1), (c, L, g, i, j)
-
-
-def _mul_rows(F, X, a, lg):
-    return X if lg == F.mod else F.mul_log(X, lg)
-
-
-def bs256_encode(F, dmat, m8e, m8d, k, p, sym):
-    """k_enc_bs256's algebra at symbol level: per chunk, IFFT layers 0, 1 (2 for
-    c = 3) with full-field twiddles in normal coordinates, the coordinate change,
-    the remaining IFFT layers as EncTab256 networks, XOR-accumulate; then FFT
-    layers 7-2 as DecTab256 networks, layers 1, 0 with subfield twiddles, the
-    coordinate change back, rows < p."""
-    M = 256
-    we, wd = widen(m8e.astype(np.uint32)), widen(m8d.astype(np.uint32))
-    acc = np.zeros((M, sym.shape[1]), np.uint32)
-    for c in range(-(-k // M)):
-        X = np.zeros((M, sym.shape[1]), np.int64)
-        n = min(M, k - M * c)
-        X[:n] = sym[M * c:M * c + n]
-        for L in _bf_layers(c):
-            for a in pairs(L, M):
-                g = a >> (L + 1)
-                lg = int(F._skew[(c + 1) * 256 - 1 + g * (2 << L) + (1 << L)])
-                X[a + (1 << L)] ^= X[a]
-                if lg != F.mod:
-                    X[a] ^= F.mul_log(X[a + (1 << L)], lg)
-        X = to_sub(dmat, X.astype(np.uint32))
-        for L in range(len(_bf_layers(c)), 8):
-            for a in pairs(L, M):
-                X[a + (1 << L)] ^= X[a]
-                X[a] ^= gf2_apply(we[c, L, a >> (L + 1)], X[a + (1 << L)])
-        acc ^= X
-    for L in range(7, 1, -1):
-        for a in pairs(L, M):
-            acc[a] ^= gf2_apply(wd[L, a >> (L + 1)], acc[a + (1 << L)])
-            acc[a + (1 << L)] ^= acc[a]
-    for L in (1, 0):
-        for a in pairs(L, M):
-            acc[a] ^= gf2_apply(wd[L, a >> (L + 1)], acc[a + (1 << L)])
-            acc[a + (1 << L)] ^= acc[a]
-    return to_sub(dmat, acc)[:p]
-
-
-@pytest.mark.parametrize("k,p", [(1024, 256), (1000, 200), (257, 129), (3, 130), (768, 256)])
-def test_bs256_schedule_matches_oracle(k, p):
-    """The m = 256 encode's layer split (byte form / networks, coordinate
-    changes, EncTab256 / DecTab256 tables) gives the oracle's parity bit for
-    bit (leopard16.go:128-224)."""
-    from oracle import leopard_np as lnp
-
-    F = lnp.field(16)
-    _, m8e, _ = load_enctab256()
-    m8d, _ = load_dectab()
-    dmat = load_tables()[5]["dmat"]
-    rng = np.random.default_rng(k + 7 * p)
-    S = 64
-    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
-    blk = data.reshape(k, -1, 64)
-    sym = (blk[:, :, :32].astype(np.uint32) | (blk[:, :, 32:].astype(np.uint32) << 8)).reshape(k, -1)
-    par = bs256_encode(F, dmat, m8e, m8d, k, p, sym).reshape(p, -1, 32)
-    got = np.concatenate([(par & 0xFF).astype(np.uint8), (par >> 8).astype(np.uint8)], axis=2).reshape(p, S)
-    assert np.array_equal(got, orc.encode(16, k, p, data)), (k, p)

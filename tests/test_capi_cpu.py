@@ -138,10 +138,7 @@ def test_constructor_errors():
     assert rs.New16(193, 16).encode_path == "split16-m16"  # 13 chunks: past the m = 16 table
     assert rs.New16(64, 8).encode_path == "split16-m8"
     assert rs.New16(10, 1).encode_path == "reg16-m1"
-    # bit-sliced m = 256 kernel: 129 <= p <= 256, k <= 4 chunks; past that the LDS kernel
-    assert rs.New16(1024, 256).encode_path == "bs16-m256"
-    assert rs.New16(200, 129).encode_path == "bs16-m256"
-    assert rs.New16(1025, 256).encode_path == "lds-m256"
+    assert rs.New16(1024, 256).encode_path == "lds-m256"
     assert rs.New16(96, 100).encode_path == "lds-m128"
     assert rs.New16(1024, 300).encode_path == "multipass"
 
