@@ -127,29 +127,6 @@ constexpr uint32_t z_after(uint32_t z, int qb) {
 // it touches in SGPRs for the whole loop (hundreds of SGPR spills).
 typedef __attribute__((address_space(4))) const RecArgs cargs_t;
 
-// RS_DEC_ABL: bitmask of steps left out (build experiments only; wrong results):
-// 1 row loads, 2 phase-1 transform, 4 phase 2, 8 phase-3 transform, 16 reveal,
-// 32 scale-in, 64 phase-1 / phase-3 byte <-> plane transposes
-#ifndef RS_DEC_ABL
-#define RS_DEC_ABL 0
-#endif
-#define ABL(b) ((RS_DEC_ABL >> (b)) & 1)
-// RS_DEC_STAMP (diagnostic builds only): per-wave cycle sums of the loop's
-// segments, written to DecPlan::stamps and printed by the launcher.
-#ifdef RS_DEC_STAMP
-#define STAMP(k)                                          \
-    do {                                                  \
-        const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
-        seg[k] += now_ - last_;                           \
-        last_ = now_;                                     \
-    } while (0)
-#else
-#define STAMP(k) \
-    do {         \
-    } while (0)
-#endif
-[[maybe_unused]] constexpr int kSegs = 16;
-
 template <bool STRIDED>
 struct Dec {
     cargs_t *ap;        // the kernel's RecArgs (first kernel argument, kernarg offset 0)
@@ -394,12 +371,12 @@ struct Dec {
             for (int b = 0; b < nbar; b++) lds_barrier();
             return;
         }
-        if constexpr (!ABL(0)) load_rows(u);
-        if constexpr (!ABL(5)) scale(u);
-        if constexpr (!ABL(1)) ifft0_bytes(u);
+        load_rows(u);
+        scale(u);
+        ifft0_bytes(u);
         for (int b = 0; b < nbar; b++) lds_barrier();
-        if constexpr (!ABL(6)) to_planes(0xFFu);
-        if constexpr (!ABL(1)) ifft_a(u);
+        to_planes(0xFFu);
+        ifft_a(u);
     }
     // V[0..7] <-> V[8..15] (the parked unit)
     __device__ __forceinline__ void park_swap() {
@@ -535,13 +512,13 @@ struct Dec {
         cargs_t &a = args();
         const Need need = load_need(a.need);
         const uint32_t nw = __builtin_amdgcn_readfirstlane(unit_need(need, u));
-        if constexpr (!ABL(3)) fft_a(u);
+        fft_a(u);
         uint32_t pairs = 0;  // register rows holding a revealed row (either z)
 #pragma unroll
         for (int i = 0; i < 8; i++) pairs |= ((nw >> (2 * i)) & 3u) ? 1u << i : 0u;
-        if constexpr (!ABL(6)) to_bytes(pairs);
+        to_bytes(pairs);
         fft0_bytes(u, nw);
-        if constexpr (!ABL(4)) reveal(u, nw, need);
+        reveal(u, nw, need);
     }
     // out = work * (mod - errLocs) for the revealed rows 16u + t (bit t of nw)
     __device__ __forceinline__ void reveal(int u, uint32_t nw, const Need &need) {
@@ -586,10 +563,7 @@ struct Dec {
 
 // Waves per workgroup: 8 run phase 2 (B layout: wave = row bits 1-3); waves
 // 8 .. kWaves-1 run phase 1 of the next tile meanwhile.  12 = three waves per SIMD.
-#ifndef RS_DEC_WAVES
-#define RS_DEC_WAVES 12
-#endif
-constexpr int kWaves = RS_DEC_WAVES;
+constexpr int kWaves = 12;
 static_assert(kWaves > 8 && kWaves <= 12, "wave count");
 constexpr int kUnits = kImgRows / 16;  // 16-row units below the image end
 
@@ -604,7 +578,6 @@ struct DecPlan {
     uint64_t code[3];  // 16 bits per wave, waves 4j .. 4j+3 in code[j]
     int ntx;           // column tiles per stripe
     int ntiles;        // column tiles x stripes
-    uint64_t *stamps;  // RS_DEC_STAMP builds: kSegs cycle sums per wave
 };
 
 // Persistent over tiles t = blockIdx.x + i * gridDim.x (column tile t % ntx of
@@ -639,10 +612,6 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
     };
     int t = -1, tn = blockIdx.x;  // tile in phases 2-3, tile in phase 1
     if (tn >= pl.ntiles) return;
-#ifdef RS_DEC_STAMP
-    uint64_t seg[kSegs] = {};
-    uint64_t last_ = __builtin_amdgcn_s_memtime();
-#endif
     for (;;) {
         const bool cur = t >= 0, more = tn < pl.ntiles;
         // The first iteration has no phase 2 / 3: every wave is free, so
@@ -679,14 +648,11 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
             }
             __builtin_amdgcn_s_setprio(0);
         }
-        STAMP(12);
         if (cur) {
             // ---- phase 2: Y = B_F (I + H) B_I u + Lo u (B layout)
             if (!early)
-                if constexpr (!ABL(2)) d.phase2();
-            STAMP(0);
+                d.phase2();
             if (!early_p1) lds_barrier();  // every wave has read u
-            STAMP(1);
             if (!early) {
                 int wt = w;
                 asm volatile("" : "+s"(wt));
@@ -694,7 +660,6 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
                 for (int q = 0; q < Dec<STRIDED>::NQ; q++) d.img_put(2 * wt + 16 * q, d.V[q]);
             }
             if (!early_p1) lds_barrier();  // Y is in the image
-            STAMP(2);
             if (p3a >= 0) {
                 // ---- phase 3 of tile t, one unit at a time (each read from the
                 // image before the barrier below frees it)
@@ -707,17 +672,14 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
                     d.phase3(u);
                 }
             }
-            STAMP(4);
         }
         if (!early && more && p1a >= 0) {
             // ---- late phase 1 of tile tn (registers only)
             set_tile(tn);
             d.phase1(p1a);
         }
-        STAMP(5);
         if (!more) break;
         lds_barrier();  // the image is free for phase 1 of tile tn
-        STAMP(3);
         if (p1a >= 0) {
             if (early) {
                 d.template unit_put<0>(p1b >= 0 ? p1b : p1a);
@@ -727,14 +689,9 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
             }
         }
         lds_barrier();  // u of tile tn is in the image
-        STAMP(6);
         t = tn;
         tn += gridDim.x;
     }
-#ifdef RS_DEC_STAMP
-    if (d.lane() == 0)
-        for (int k = 0; k < kSegs; k++) pl.stamps[((uint64_t)blockIdx.x * kWaves + w) * kSegs + k] = seg[k];
-#endif
 }
 
 // Unit placement (see DecPlan).  VALU cost: a phase-1 unit 2, a phase-3 unit
@@ -759,7 +716,7 @@ DecPlan make_plan(const RecArgs &a) {
         auto it = cache.find(key);
         if (it != cache.end()) return it->second;
     }
-    // Cost model (cycles per tile, from RS_DEC_STAMP runs at C4): a phase-1
+    // Cost model (cycles per tile, from per-wave s_memtime stamps of lab builds at C4, scripts/lab): a phase-1
     // unit 27 k (a unit past mtrunc only writes zeros: 1 k), a phase-3 unit
     // 14 k, phase 2 plus the exchange 17 k before a wave < 8 starts its units;
     // the early waves start at once.  E phase-1 units go to the early waves
@@ -859,36 +816,8 @@ hipError_t launch_rec_bs256(const RecArgs &a, hipStream_t s) {
     if ((uint64_t)pl.ntx * ny > (uint64_t)INT32_MAX) return hipErrorInvalidValue;
     pl.ntiles = (int)(pl.ntx * ny);
     const unsigned grid = (unsigned)std::min<int>(pl.ntiles, std::max(cus, 1));
-#ifdef RS_DEC_STAMP
-    static uint64_t *dstamps = nullptr;
-    static int nprint = 0;
-    const size_t nst = (size_t)grid * kWaves * kSegs;
-    if (!dstamps && hipMalloc(&dstamps, 4096 * 16 * kSegs * sizeof(uint64_t)) != hipSuccess) return hipErrorOutOfMemory;
-    (void)hipMemsetAsync(dstamps, 0, nst * sizeof(uint64_t), s);
-    pl.stamps = dstamps;
-#endif
     if (a.base) hipLaunchKernelGGL(k_rec_bs256<true>, dim3(grid), dim3(64 * kWaves), 0, s, a, pl);
     else hipLaunchKernelGGL(k_rec_bs256<false>, dim3(grid), dim3(64 * kWaves), 0, s, a, pl);
-#ifdef RS_DEC_STAMP
-    if (nprint < 4 && pl.ntiles >= 1024) {
-        nprint++;
-        std::vector<uint64_t> h(nst);
-        (void)hipStreamSynchronize(s);
-        (void)hipMemcpy(h.data(), dstamps, nst * sizeof(uint64_t), hipMemcpyDeviceToHost);
-        std::fprintf(stderr, "stamps: grid %u tiles %d plan %016llx %016llx %016llx (mean cycles per workgroup)\n", grid,
-                     pl.ntiles, (unsigned long long)pl.code[0], (unsigned long long)pl.code[1],
-                     (unsigned long long)pl.code[2]);
-        for (int w = 0; w < kWaves; w++) {
-            std::fprintf(stderr, "  wave %d:", w);
-            for (int k = 0; k < kSegs; k++) {
-                double m = 0;
-                for (unsigned b = 0; b < grid; b++) m += (double)h[((size_t)b * kWaves + w) * kSegs + k];
-                std::fprintf(stderr, " %7.0f", m / grid);
-            }
-            std::fprintf(stderr, "\n");
-        }
-    }
-#endif
     return hipGetLastError();
 }
 

@@ -453,7 +453,7 @@ int scratch_ensure(rs_codec *c, DevBuf<T> &b, size_t want) {
 
 // Data rows [0,k) and parity rows [k,k+p) as RowSets: strided when both sets'
 // pointers are equally spaced (AllocAligned slab), else both via a device
-// table (one strided set and one table would reach a kernel whose TABLE
+// table (one strided set and one table would reach a kernel whose ROWTAB
 // parameter covers both: a null table dereference).
 int make_rowsets(rs_codec *c, uint8_t *const *d, hipStream_t s, RowSet &data, RowSet &par) {
     auto strided = [&](int lo, int cnt, RowSet &rs) {
@@ -477,7 +477,7 @@ int make_rowsets(rs_codec *c, uint8_t *const *d, hipStream_t s, RowSet &data, Ro
         HIP_TRY(hipMemcpy(c->rows.p, tbl.data(), c->total * sizeof(uint8_t *), hipMemcpyHostToDevice));
         c->rows_host = tbl;
     }
-    // both sets from the table: the kernels take one layout (template TABLE)
+    // both sets from the table: the kernels take one layout (template ROWTAB)
     // for data and parity rows alike
     data = RowSet{c->rows.p, nullptr, 0};
     par = RowSet{c->rows.p + c->k, nullptr, 0};

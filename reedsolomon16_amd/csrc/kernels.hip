@@ -502,9 +502,9 @@ __device__ __forceinline__ uint32_t vgpr_lds_addr(const uint8_t *p) {
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 
-template <bool TABLE>
+template <bool ROWTAB>
 __device__ __forceinline__ uint8_t *rowp(const RowSet &rs, int i, uint64_t soff) {
-    if constexpr (TABLE) return rs.table[i];
+    if constexpr (ROWTAB) return rs.table[i];
     else return rs.base + (uint64_t)i * rs.stride + soff;
 }
 
@@ -515,7 +515,7 @@ __device__ __forceinline__ uint8_t *rowp(const RowSet &rs, int i, uint64_t soff)
 // the wave's private image, and its twiddle tables into the block's other
 // table buffer.  HBM sees exactly k row reads and p row writes (p reads for
 // verify) per unit.
-template <class F, int LOGM, bool VERIFY, bool TABLE>
+template <class F, int LOGM, bool VERIFY, bool ROWTAB>
 __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
     constexpr int M = 1 << LOGM;
     constexpr int ROWB = F::ROWB;          // bytes of a row covered by one wave
@@ -545,8 +545,8 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
     // Buffer descriptor over this stripe's data rows (strided mode; the host
     // guarantees (k-1)*stride + shard_size < 2^32).
     const __amdgpu_buffer_rsrc_t drsrc = __builtin_amdgcn_make_buffer_rsrc(
-        TABLE ? nullptr : (void *)(a.data.base + soff), 0,
-        TABLE ? 0 : (int)(uint32_t)((uint64_t)(a.k - 1) * a.data.stride + a.shard_size), 0x00020000);
+        ROWTAB ? nullptr : (void *)(a.data.base + soff), 0,
+        ROWTAB ? 0 : (int)(uint32_t)((uint64_t)(a.k - 1) * a.data.stride + a.shard_size), 0x00020000);
     // One DMA wave-instruction (piece group j) of chunk c's rows.
     auto stage_one = [&](int c, int j) {
         const int row0 = c * M, cnt = a.k - row0;
@@ -555,8 +555,8 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
             const int r = P / PPR;
             const uint64_t go = span + F::piece_goff(P % PPR);
             if (wave_live && r < cnt && go < a.shard_size) {
-                if constexpr (TABLE) {
-                    const uint8_t *src = rowp<TABLE>(a.data, row0 + r, soff) + go;
+                if constexpr (ROWTAB) {
+                    const uint8_t *src = rowp<ROWTAB>(a.data, row0 + r, soff) + go;
                     __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(img + j * 1024), 16, 0, 0);
                 } else {
                     // MUBUF LDS-DMA: with a FLAT global_load_lds in flight the compiler's
@@ -624,12 +624,12 @@ __global__ void __launch_bounds__(256, 2) k_encode_reg(EncodeArgs a) {
         uint32_t bad = 0;
 #pragma unroll
         for (int r = 0; r < M; r++)
-            if (r < a.p) bad |= F::diff(acc[r], F::load(rowp<TABLE>(a.parity, r, soff), u));
+            if (r < a.p) bad |= F::diff(acc[r], F::load(rowp<ROWTAB>(a.parity, r, soff), u));
         flag_mismatch(a.mismatch, bad != 0);
     } else {
 #pragma unroll
         for (int r = 0; r < M; r++)
-            if (r < a.p) F::store(rowp<TABLE>(a.parity, r, soff), u, acc[r]);
+            if (r < a.p) F::store(rowp<ROWTAB>(a.parity, r, soff), u, acc[r]);
     }
 }
 
