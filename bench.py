@@ -138,8 +138,9 @@ def other_workloads(torch, rs, dev, stream) -> dict:
     """Kernel time of the other BASELINE configs on this GPU, beside the
     headline (reported, not the metric): C4 = reconstruct of 128+32 x 1 MiB
     with 32 erased shards, 16 stripes per launch (rs_reconstruct_dev_batch);
-    C5 = encode of 1024+256 x 256 KiB, 32 stripes per launch.  Algorithmic
-    bytes: rows read + rows written per stripe (C4: 128 + 32, C5: 1024 + 256)."""
+    C5 = encode of 1024+256 x 256 KiB, 32 stripes per launch, and its repair
+    with 256 erased shards, 8 stripes per launch.  Algorithmic bytes: rows
+    read + rows written per stripe (C4: 128 + 32, C5: 1024 + 256)."""
     import numpy as np
 
     out = {}
@@ -178,6 +179,16 @@ def other_workloads(torch, rs, dev, stream) -> dict:
     out["C5_encode"] = {"config": "1024+256 x 256 KiB, 32 stripes per launch", "kernel_path": c5.encode_path,
                         "kernel_ms": round(ms, 5), "us_per_stripe": round(ms * 1e3 / ns, 2),
                         "alg_bytes_per_launch": alg, "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    # the C5 repair: 256 erased shards (n = 2048 work rows), 8 stripes of the slab
+    ns = 8
+    c5.encode_dev_batch(slab[:ns], stream)
+    present = np.ones(k + p, bool)
+    present[np.random.default_rng(0xC5).choice(k + p, p, replace=False)] = False
+    ms = kernel_ms(lambda: c5.reconstruct_dev_batch(slab[:ns], present, stream=stream), 5)
+    alg = ns * (k + p) * S
+    out["C5_reconstruct"] = {"config": "1024+256 x 256 KiB, 256 erased shards, 8 stripes per launch",
+                             "kernel_ms": round(ms, 5), "us_per_stripe": round(ms * 1e3 / ns, 2),
+                             "alg_bytes_per_launch": alg, "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
     del slab
     torch.cuda.empty_cache()
     return out
