@@ -138,6 +138,50 @@ __global__ void __launch_bounds__(256) k_tile_pieces(uint8_t *base, uint32_t RS,
     }
 }
 
+// The engine's memory schedule in isolation (k_encode_hp, m = 32): a 2 KB tile
+// per 256-thread workgroup, every lane owning 64-byte block b = lane & 31 of
+// rows 4h + i of its wave's 8-row group (h = lane >> 5); four chunks of 32
+// rows, each chunk's 16 row loads per lane (4 rows x 4 x 16 B) in registers
+// before they are folded into the accumulator, then 32 parity rows stored
+// per tile.  KL = 1: the engine's lane layout (each load instruction touches
+// 16 B of every 64-byte block: 16 bytes at a 64-byte lane stride); KL = 0:
+// the same bytes per lane group but each instruction lane-contiguous (a lane
+// takes 16-byte piece l of a 1 KB run).  Occupancy fixed by dynamic LDS.
+template <bool KL, bool KLS = KL>
+__global__ void __launch_bounds__(256) k_engine_mem(uint8_t *base, uint32_t RS, uint64_t SS) {
+    const int tps = S / 2048;
+    const int stripe = blockIdx.x / tps, ct = blockIdx.x - stripe * tps;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)stripe * SS, 0, (int)((K + P) * RS), 0x00020000);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, b = lane & 31;
+    u32x4 acc[4][4] = {};
+    for (int c = 0; c < 4; c++) {
+        u32x4 v[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t row = (uint32_t)(32 * c + 8 * w + 4 * h + i);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                // KL: lane b, piece q of its block; else: piece (lane & 31) of 1 KB run (q & 1) of row-pair half
+                const uint32_t col = KL ? (uint32_t)ct * 2048 + b * 64 + q * 16 : (uint32_t)ct * 2048 + (q >> 1) * 1024 + (q & 1) * 512 + b * 16;
+                v[i][q] = ldx<false>(rs, col, row * RS);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc[i][q] ^= v[i][q];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t row = (uint32_t)(K + 8 * w + 4 * h + i);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t col = KLS ? (uint32_t)ct * 2048 + b * 64 + q * 16 : (uint32_t)ct * 2048 + (q >> 1) * 1024 + (q & 1) * 512 + b * 16;
+            __builtin_amdgcn_raw_buffer_store_b128(acc[i][q], rs, col, row * RS, 0);
+        }
+    }
+}
+
 // Plain 4:1 one-shot stream: block b reads U float4 per lane from each of 4
 // regions and writes their XOR to the destination.
 template <int U, bool NT>
@@ -219,6 +263,14 @@ int main(int argc, char **argv) {
         TILEO(512, 64, 40);
         TILEO(512, 128, 40);
         TILEO(512, 256, 64);
+        {
+            const unsigned g = (unsigned)((uint64_t)nst * (S / 2048));
+            rep("engine memory schedule, KL loads/stores, 64 KB LDS", timeit([&] { hipLaunchKernelGGL((k_engine_mem<true>), dim3(g), dim3(256), 64 << 10, 0, slab, RS, SS); }), alg);
+            rep("engine memory schedule, contiguous, 64 KB LDS", timeit([&] { hipLaunchKernelGGL((k_engine_mem<false>), dim3(g), dim3(256), 64 << 10, 0, slab, RS, SS); }), alg);
+            rep("engine memory schedule, KL loads, contiguous stores", timeit([&] { hipLaunchKernelGGL((k_engine_mem<true, false>), dim3(g), dim3(256), 64 << 10, 0, slab, RS, SS); }), alg);
+            rep("engine memory schedule, contiguous loads, KL stores", timeit([&] { hipLaunchKernelGGL((k_engine_mem<false, true>), dim3(g), dim3(256), 64 << 10, 0, slab, RS, SS); }), alg);
+            rep("engine memory schedule, KL loads/stores, no LDS", timeit([&] { hipLaunchKernelGGL((k_engine_mem<true>), dim3(g), dim3(256), 0, 0, slab, RS, SS); }), alg);
+        }
         TILE(512, 256, false, 1);
         TILE(512, 256, true, 1);
         {
