@@ -151,6 +151,10 @@ struct rs_codec {
     // and the coordinate-change map (EncodeArgs::tw_fft_sub / tw_dmap)
     DevBuf<uint32_t> tw_fft_sub, tw_dmap;
     bool fft_sub = false;  // its twiddle images (schedule.hpp EncodeSplit)
+    // ... and the chunk IFFT passes from ifft_nff[c] on (EncodeArgs::tw_ifft_sub)
+    DevBuf<uint32_t> tw_ifft_sub;
+    DevBuf<int> ifft_nff;
+    bool ifft_sub = false;
     std::string path;
 
     // decode plan (built on first reconstruct)
@@ -227,7 +231,7 @@ struct rs_codec {
             (void)hipEventSynchronize(scratch_ev);
             (void)hipEventDestroy(scratch_ev);
         }
-        tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); tw_fft_sub.release(); tw_dmap.release(); dtw_ifft.release(); dtw_fft.release();
+        tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); tw_fft_sub.release(); tw_dmap.release(); tw_ifft_sub.release(); ifft_nff.release(); dtw_ifft.release(); dtw_fft.release();
         work.release(); rows.release();
         if (hflag) (void)hipHostFree(hflag);
         if (dflag) (void)hipFree(dflag);
@@ -344,6 +348,37 @@ void plan_encode_host(rs_codec *c) {
     if (c->bs_ok) c->path = std::string("bs16-m") + std::to_string(c->m);
 }
 
+// Chunk IFFT passes of the LDS encode in subfield coordinates (EncodeArgs::
+// tw_ifft_sub): chunk c's twiddles are fftSkew[(c+1)m - 1 + ...]
+// (ifftDITEncoder leopard16.go:699-741), full-field in the first layers and
+// in GF(2^8) after them (C5, m = 256: layers 0-1 of every chunk and layer 2
+// of chunk 3 are full-field).  ifft_nff[c] = the first radix-4 pass from which
+// every slot of the chunk lies in the subfield; the kernel needs the last
+// pass subfield (it is fused with the accumulator).
+int upload_ifft_sub(rs_codec *c) {
+    const auto passes = ifft_passes(c->logm);
+    const int np = (int)passes.size(), is = ifft_slots(c->logm);
+    for (const PassInfo &ps : passes)
+        if (ps.radix != 4) return RS_OK;
+    std::vector<int> nff(c->nchunks, 1);
+    std::vector<uint32_t> ts((size_t)c->nchunks * is * kTwDwords8, 0);
+    for (int ch = 0; ch < c->nchunks; ch++) {
+        const uint32_t *lg = c->enc_ifft_logs.data() + (size_t)ch * is;
+        for (int p = 0; p < np; p++)
+            for (int sl = passes[p].slot_off; sl < passes[p].slot_off + 3 * passes[p].groups; sl++)
+                if (lg[sl] != c->F->mod && !in_subfield(*c->F, lg[sl])) nff[ch] = std::max(nff[ch], p + 1);
+        if (nff[ch] > 2 || nff[ch] >= np) return RS_OK;  // the kernel compiles nff = 1 and 2
+        for (int sl = passes[nff[ch]].slot_off; sl < is; sl++)
+            make_sub_twiddle(*c->F, lg[sl], ts.data() + ((size_t)ch * is + sl) * kTwDwords8);
+    }
+    HIP_TRY(c->tw_ifft_sub.ensure(ts.size()));
+    HIP_TRY(c->ifft_nff.ensure(nff.size()));
+    HIP_TRY(hipMemcpy(c->tw_ifft_sub.p, ts.data(), ts.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->ifft_nff.p, nff.data(), nff.size() * sizeof(int), hipMemcpyHostToDevice));
+    c->ifft_sub = true;
+    return RS_OK;
+}
+
 // Device half, on first use: stream, flag word, encode twiddle tables.
 int ensure_device(rs_codec *c) {
     if (c->dev_ready) return RS_OK;
@@ -374,6 +409,7 @@ int ensure_device(rs_codec *c) {
             HIP_TRY(hipMemcpy(c->tw_fft_sub.p, hf.data(), hf.size() * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(c->tw_dmap.p, dm.data(), dm.size() * 4, hipMemcpyHostToDevice));
             c->fft_sub = true;
+            if (int e2 = upload_ifft_sub(c)) return e2;
         }
     }
     c->dev_ready = true;
@@ -575,6 +611,10 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
         if (c->fft_sub) {
             a.tw_fft_sub = c->tw_fft_sub.p;
             a.tw_dmap = c->tw_dmap.p;
+            if (c->ifft_sub) {
+                a.tw_ifft_sub = c->tw_ifft_sub.p;
+                a.ifft_nff = c->ifft_nff.p;
+            }
         }
         a.mismatch = mismatch;
         HIP_TRY(launch_encode_lds(c->bits, c->logm, mismatch != nullptr, a, s));

@@ -1172,7 +1172,9 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
 // first pass reads through `in`, the last writes through `out`.  A first pass
 // that does not read the LDS image runs every group (rows past mtrunc come in
 // as zero, and zero rows transform to zero rows): later passes read those rows.
-template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed, int P0 = 0, int P1 = 32, int NT = 256>
+// OUT_P1: pass P1 - 1 (the last this call runs) writes through `out` too.
+template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed, int P0 = 0, int P1 = 32, int NT = 256,
+          bool OUT_P1 = false>
 __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
                                               NeedT need, const In &in, const Out &out) {
     constexpr int N = 1 << LOGN, NP4 = LOGN / 2, NP = NP4 + (LOGN & 1);
@@ -1212,10 +1214,11 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
             if constexpr (INV) lds_pass<F, INV, std::decay_t<decltype(pin)>, std::decay_t<decltype(pout)>, NoNeed, NT>(dist, radix4 ? 4 : 2, active, t, NoNeed{}, pin, pout);
             else lds_pass<F, INV, std::decay_t<decltype(pin)>, std::decay_t<decltype(pout)>, NeedT, NT>(dist, radix4 ? 4 : 2, active, t, need, pin, pout);
         };
+        constexpr bool to_out = p == NP - 1 || (OUT_P1 && p == P1 - 1);
         if constexpr (from_hbm) {
-            if constexpr (p == NP - 1) run(in, out);
+            if constexpr (to_out) run(in, out);
             else run(in, lio);
-        } else if constexpr (p == NP - 1) {
+        } else if constexpr (to_out) {
             run(lio, out);
         } else {
             run(lio, lio);
@@ -1391,8 +1394,21 @@ __device__ __forceinline__ void sub_swap(typename F::Vec &v, const uint32_t *__r
     }
 }
 
+// LDS sink that changes rows into subfield coordinates on their way in.
+template <class F>
+struct LdsPsi {
+    uint8_t *lds;
+    const uint32_t *dmap;
+    __device__ void operator()(int row, int u, const typename F::Vec &v0) const {
+        typename F::Vec v = v0;
+        sub_swap<F>(v, dmap);
+        LTile<F>::put(lds, row, u, v);
+    }
+};
+
 // FT: the field of the final FFT (F16S: subfield coordinates, EncodeArgs::tw_fft_sub).
-template <class F, int LOGM, bool VERIFY, class FT = F>
+// ISUB: the chunk IFFTs' subfield passes (EncodeArgs::tw_ifft_sub; needs FT = F16S).
+template <class F, int LOGM, bool VERIFY, class FT = F, bool ISUB = false>
 __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
@@ -1447,12 +1463,29 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
             return sl;
         }();
         V ar[KF][4];
+        // chunk IFFT passes in subfield coordinates from ifft_nff[c] on
+        // (6 v_perm_b32 per product instead of 12; EncodeArgs::tw_ifft_sub)
+        constexpr bool isub = SUB && ISUB;
         for (int c = 0; c < a.nchunks; c++) {
             const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
             const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
+            const uint32_t *tws = isub ? a.tw_ifft_sub + (uint64_t)c * its * FT::TWD : nullptr;
             const LdsIO<F> lio{cur};
             const ChunkIn in{a, row0, cnt, soff, tile};
-            lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, NP - 1>(cur, cnt, tw, NoNeed{}, in, lio);
+            if constexpr (isub) {
+                // full-field passes, the last one writing subfield coordinates, then subfield passes
+                const LdsPsi<F> psi{cur, a.tw_dmap};
+                const LdsIO<FT> lios{cur};
+                if (a.ifft_nff[c] == 1) {
+                    lds_transform<F, true, LOGM, ChunkIn, LdsPsi<F>, NoNeed, 0, 1, 256, true>(cur, cnt, tw, NoNeed{}, in, psi);
+                    lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 1, NP - 1>(cur, cnt, tws, NoNeed{}, lios, lios);
+                } else {
+                    lds_transform<F, true, LOGM, ChunkIn, LdsPsi<F>, NoNeed, 0, 2, 256, true>(cur, cnt, tw, NoNeed{}, in, psi);
+                    lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 2, NP - 1>(cur, cnt, tws, NoNeed{}, lios, lios);
+                }
+            } else {
+                lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, NP - 1>(cur, cnt, tw, NoNeed{}, in, lio);
+            }
 #pragma unroll
             for (int k = 0; k < KF; k++) {
                 const int it = threadIdx.x + 256 * k;
@@ -1461,7 +1494,8 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
                     V x[4];
 #pragma unroll
                     for (int q = 0; q < 4; q++) x[q] = L::get(cur, i + q * D, u);
-                    ifft4<F>(x[0], x[1], x[2], x[3], tw + (uint64_t)last * F::TWD);
+                    if constexpr (isub) ifft4<FT>(x[0], x[1], x[2], x[3], tws + (uint64_t)last * FT::TWD);
+                    else ifft4<F>(x[0], x[1], x[2], x[3], tw + (uint64_t)last * F::TWD);
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
                         if (c == 0) ar[k][q] = x[q];
@@ -1478,9 +1512,9 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
             const int it = threadIdx.x + 256 * k;
             if (it < D * L::U) {
                 const int i = it / L::U, u = it - i * L::U;
-                if constexpr (SUB)
+                if constexpr (SUB && !isub)  // (a subfield IFFT leaves acc in subfield coordinates already)
 #pragma unroll
-                    for (int q = 0; q < 4; q++) sub_swap<F>(ar[k][q], a.tw_dmap);  // into subfield coordinates
+                        for (int q = 0; q < 4; q++) sub_swap<F>(ar[k][q], a.tw_dmap);  // into subfield coordinates
                 fft4<FT>(ar[k][0], ar[k][1], ar[k][2], ar[k][3], twf);
 #pragma unroll
                 for (int q = 0; q < 4; q++) L::put(cur, i + q * D, u, ar[k][q]);
@@ -1547,13 +1581,21 @@ template <class F, int LOGM, class FT>
 hipError_t enc_lds_tt(bool verify, const EncodeArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)((a.shard_size + LTile<F>::TB - 1) / LTile<F>::TB), (unsigned)a.nstripes);
     const size_t lds = (size_t)(enc_acc_regs(LOGM) ? 1 : 2) * (1 << LOGM) * LTile<F>::ROW;
-    if (verify) {
-        (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, true, FT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((k_enc_lds<F, LOGM, true, FT>), grid, dim3(256), lds, s, a);
-    } else {
-        (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, false, FT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((k_enc_lds<F, LOGM, false, FT>), grid, dim3(256), lds, s, a);
+    auto go = [&](auto vf, auto sf) {
+        constexpr bool V = decltype(vf)::value, IS = decltype(sf)::value;
+        (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, V, FT, IS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_enc_lds<F, LOGM, V, FT, IS>), grid, dim3(256), lds, s, a);
+    };
+    const bool isub = !std::is_same<F, FT>::value && a.tw_ifft_sub && a.ifft_nff;
+    if constexpr (!std::is_same<F, FT>::value) {
+        if (isub) {
+            if (verify) go(std::true_type{}, std::true_type{});
+            else go(std::false_type{}, std::true_type{});
+            return hipGetLastError();
+        }
     }
+    if (verify) go(std::true_type{}, std::false_type{});
+    else go(std::false_type{}, std::false_type{});
     return hipGetLastError();
 }
 template <class F>

@@ -38,6 +38,13 @@ struct EncodeArgs {
     // instead of 12); tw_dmap is the byte map D (make_sub_dmap).  nullptr: full field.
     const uint32_t *tw_fft_sub;
     const uint32_t *tw_dmap;
+    // Optional (with tw_fft_sub): chunk c's IFFT passes from ifft_nff[c] on in
+    // subfield coordinates too (tw_ifft_sub: nchunks x ifft_slots(logm)
+    // kTwDwords8 tables, zero where a slot is full-field): the passes before it
+    // run full-field and the last of them changes coordinates on its way into
+    // the LDS image.  Every later slot of the chunk lies in GF(2^8).
+    const uint32_t *tw_ifft_sub;
+    const int *ifft_nff;
 };
 
 // Returns hipSuccess or the launch error.  logm in [0, 5].
