@@ -162,6 +162,10 @@ struct rs_codec {
     bool dec_sub = false;  // LDS reconstruct runs its transforms in subfield coordinates
     int n = 0, logn = 0;
     DevBuf<uint32_t> dtw_ifft, dtw_fft;
+    // n = 512..2048: subfield tables of the passes that run in subfield
+    // coordinates (RecArgs::tw_ifft_sub / tw_fft_sub, kernels.hip BigSub)
+    bool dec_big_sub = false;
+    DevBuf<uint32_t> dtw_ifft_sub, dtw_fft_sub, dec_dmap;
 
     // scratch shared by the codec's calls (row table, multi-pass work rows,
     // reconstruct blob).  Calls may run on different caller streams and the
@@ -231,7 +235,7 @@ struct rs_codec {
             (void)hipEventSynchronize(scratch_ev);
             (void)hipEventDestroy(scratch_ev);
         }
-        tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); tw_fft_sub.release(); tw_dmap.release(); tw_ifft_sub.release(); ifft_nff.release(); dtw_ifft.release(); dtw_fft.release();
+        tw_ifft.release(); tw_fft.release(); tws_ifft.release(); tws_fft.release(); tw_fft_sub.release(); tw_dmap.release(); tw_ifft_sub.release(); ifft_nff.release(); dtw_ifft.release(); dtw_fft.release(); dtw_ifft_sub.release(); dtw_fft_sub.release(); dec_dmap.release();
         work.release(); rows.release();
         if (hflag) (void)hipHostFree(hflag);
         if (dflag) (void)hipFree(dflag);
@@ -416,6 +420,46 @@ int ensure_device(rs_codec *c) {
     return RS_OK;
 }
 
+// n = 512..2048 (GF(2^16)): the decoder layers with a full-field twiddle are
+// 0 (n = 512), 0-1 (1024) and 0-2 (2048), fftSkew indices >= 255 everywhere
+// else lying in GF(2^8) all the same; so the IFFT runs its passes from NI on
+// (NI = 2 at n = 2048, else 1) and the FFT its first FEND = 4 passes in
+// subfield coordinates (kernels.hip BigSub).  Checked against the
+// schedule's own logs: a codec whose slots do not fit stays full-field.
+int upload_big_sub(rs_codec *c, const std::vector<uint32_t> &il, const std::vector<uint32_t> &fl) {
+    if (c->bits != 16 || c->logn < 9 || c->logn > kMaxLdsRecLogN16 || !sub_enabled() || !sub_coords().ok) return RS_OK;
+    const int ni = c->logn == 11 ? 2 : 1, fend = 4;
+    const auto ip = ifft_passes(c->logn), fp = fft_passes(c->logn);
+    auto range = [](const std::vector<PassInfo> &ps, int p, size_t total) {
+        return std::make_pair((size_t)ps[p].slot_off, p + 1 < (int)ps.size() ? (size_t)ps[p + 1].slot_off : total);
+    };
+    if ((int)fp.size() <= fend || (int)ip.size() <= ni) return RS_OK;
+    std::vector<uint32_t> hi(il.size() * kTwDwords8, 0), hf(fl.size() * kTwDwords8, 0), dm(kTwDwords8, 0);
+    for (int p = ni; p < (int)ip.size(); p++) {
+        const auto r = range(ip, p, il.size());
+        for (size_t sl = r.first; sl < r.second; sl++) {
+            if (!in_subfield(*c->F, il[sl])) return RS_OK;
+            make_sub_twiddle(*c->F, il[sl], hi.data() + sl * kTwDwords8);
+        }
+    }
+    for (int p = 0; p < fend; p++) {
+        const auto r = range(fp, p, fl.size());
+        for (size_t sl = r.first; sl < r.second; sl++) {
+            if (!in_subfield(*c->F, fl[sl])) return RS_OK;
+            make_sub_twiddle(*c->F, fl[sl], hf.data() + sl * kTwDwords8);
+        }
+    }
+    make_sub_dmap(dm.data());
+    HIP_TRY(c->dtw_ifft_sub.ensure(hi.size()));
+    HIP_TRY(c->dtw_fft_sub.ensure(hf.size()));
+    HIP_TRY(c->dec_dmap.ensure(dm.size()));
+    HIP_TRY(hipMemcpy(c->dtw_ifft_sub.p, hi.data(), hi.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->dtw_fft_sub.p, hf.data(), hf.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->dec_dmap.p, dm.data(), dm.size() * 4, hipMemcpyHostToDevice));
+    c->dec_big_sub = true;
+    return RS_OK;
+}
+
 int build_decode_plan(rs_codec *c) {
     if (c->dec_built) return RS_OK;
     std::vector<uint32_t> il, fl;
@@ -441,7 +485,9 @@ int build_decode_plan(rs_codec *c) {
     }
     int e = upload_twiddles(c, il, c->dtw_ifft);
     if (e) return e;
-    return upload_twiddles(c, fl, c->dtw_fft);
+    e = upload_twiddles(c, fl, c->dtw_fft);
+    if (e) return e;
+    return upload_big_sub(c, il, fl);
 }
 
 // One LDS-resident reconstruct launch covers n <= 256 (both fields) and, for
@@ -786,6 +832,13 @@ int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipS
     return RS_OK;
 }
 
+void set_big_sub(const rs_codec *c, RecArgs &ra) {
+    if (!c->dec_big_sub) return;
+    ra.tw_ifft_sub = c->dtw_ifft_sub.p;
+    ra.tw_fft_sub = c->dtw_fft_sub.p;
+    ra.tw_dmap = c->dec_dmap.p;
+}
+
 // Device-resident plan for (present, recover_all), built and uploaded on first use.
 int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, DevPlan **out) {
     std::vector<uint8_t> key(present);
@@ -859,6 +912,7 @@ int launch_rec_plan(rs_codec *c, DevPlan *dpl, uint8_t *base, uint64_t stride, u
     std::memcpy(ra.need, dpl->need, sizeof(ra.need));
     ra.need_w = dpl->need_w;
     ra.rev = dpl->rev;
+    set_big_sub(c, ra);
     ra.base = base;
     ra.stride = stride;
     ra.stripe_stride = stripe_stride;
@@ -896,6 +950,7 @@ int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uin
     std::memcpy(ra.need, dp->need, sizeof(ra.need));
     ra.need_w = dp->need_w;
     ra.rev = dp->rev;
+    set_big_sub(c, ra);
     {
         // strided: every shard the launch touches at d[0] + i * stride
         int i0 = -1, i1 = -1;

@@ -1232,6 +1232,29 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
     lds_transform<F, INV, LOGN>(lds, mtrunc, tw, NoNeed{}, lio, lio);
 }
 
+// (lo, hi) <-> (lo ^ D(hi), hi) on every symbol of v (t: make_sub_dmap table).
+template <class F>
+__device__ __forceinline__ void sub_swap(typename F::Vec &v, const uint32_t *__restrict__ t) {
+#pragma unroll
+    for (int i = 0; i < F::W; i++) {
+        const uint32_t h = v.h[i];
+        v.l[i] = xor3(v.l[i] ^ perm(t[1], t[0], h & 0x07070707u), perm(t[3], t[2], (h >> 3) & 0x07070707u),
+                      perm(t[4], t[4], (h >> 6) & 0x03030303u));
+    }
+}
+
+// LDS sink that changes rows into subfield coordinates on their way in.
+template <class F>
+struct LdsPsi {
+    uint8_t *lds;
+    const uint32_t *dmap;
+    __device__ void operator()(int row, int u, const typename F::Vec &v0) const {
+        typename F::Vec v = v0;
+        sub_swap<F>(v, dmap);
+        LTile<F>::put(lds, row, u, v);
+    }
+};
+
 // Reconstruct (leopard16.go:432-568) of one stripe, one 32W-byte tile (LTile) per workgroup.
 // F scales rows in and out (full-field tables); FT runs the transforms (F, or
 // F16S when every transform twiddle lies in GF(2^8)).  The scale-in feeds the
@@ -1241,7 +1264,14 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
 // leaves room for one or two workgroups per CU: 16 waves keep the SIMDs fed).
 template <int LOGN> constexpr int rec_lds_threads() { return LOGN >= 10 ? 1024 : 256; }
 
-template <class F, class FT, int LOGN>
+// n = 512..2048 with BSUB: the transforms in subfield coordinates wherever
+// every twiddle of a pass lies in GF(2^8) (rec_big_sub_passes; RecArgs::tw_*_sub).
+template <int LOGN> struct BigSub {
+    static constexpr int NI = LOGN == 11 ? 2 : 1;  // IFFT passes [NI, end) subfield
+    static constexpr int FEND = 4;                 // FFT passes [0, FEND) subfield
+};
+
+template <class F, class FT, int LOGN, bool BSUB = false>
 __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
@@ -1300,7 +1330,16 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
         }
     };
     const LdsIO<FT> lio{lds};
-    lds_transform<FT, true, LOGN, ScaleIn, LdsIO<FT>, NoNeed, 0, 32, NT>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
+    typedef F16S<F::W> FS;  // (BSUB only)
+    if constexpr (BSUB) {
+        // full-field passes, the last one writing subfield coordinates, then subfield passes
+        lds_transform<F, true, LOGN, ScaleIn, LdsPsi<F>, NoNeed, 0, BigSub<LOGN>::NI, NT, true>(
+            lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, LdsPsi<F>{lds, a.tw_dmap});
+        lds_transform<FS, true, LOGN, LdsIO<FS>, LdsIO<FS>, NoNeed, BigSub<LOGN>::NI, 32, NT>(
+            lds, a.mtrunc, a.tw_ifft_sub, NoNeed{}, LdsIO<FS>{lds}, LdsIO<FS>{lds});
+    } else {
+        lds_transform<FT, true, LOGN, ScaleIn, LdsIO<FT>, NoNeed, 0, 32, NT>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
+    }
     const Reveal rv{a, tile, sbase, need_of()};
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
     if constexpr (LOGN >= 3) {
@@ -1327,7 +1366,8 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
                     for (int b = 1; b < D; b <<= 1)
                         if (!(i & b)) F::xor_into(x[k][q], L::get(lds, (i | b) + q * D, u));
                 }
-                fft4<FT>(x[k][0], x[k][1], x[k][2], x[k][3], a.tw_fft);
+                if constexpr (BSUB) fft4<FS>(x[k][0], x[k][1], x[k][2], x[k][3], a.tw_fft_sub);
+                else fft4<FT>(x[k][0], x[k][1], x[k][2], x[k][3], a.tw_fft);
             }
         }
         __syncthreads();
@@ -1342,9 +1382,24 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
         }
         __syncthreads();
         if (a.prune) {
-            lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NeedT, 1, 32, NT>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
+            if constexpr (BSUB) {
+                // subfield passes up to FEND, the last one writing normal coordinates back, then full-field
+                lds_transform<FS, false, LOGN, LdsIO<FS>, LdsPsi<F>, NeedT, 1, BigSub<LOGN>::FEND, NT, true>(
+                    lds, a.mtrunc, a.tw_fft_sub, need_of(), LdsIO<FS>{lds}, LdsPsi<F>{lds, a.tw_dmap});
+                lds_transform<F, false, LOGN, LdsIO<F>, Reveal, NeedT, BigSub<LOGN>::FEND, 32, NT>(
+                    lds, a.mtrunc, a.tw_fft, need_of(), LdsIO<F>{lds}, rv);
+            } else {
+                lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NeedT, 1, 32, NT>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
+            }
         } else {
-            lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NoNeed, 1, 32, NT>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
+            if constexpr (BSUB) {
+                lds_transform<FS, false, LOGN, LdsIO<FS>, LdsPsi<F>, NoNeed, 1, BigSub<LOGN>::FEND, NT, true>(
+                    lds, a.mtrunc, a.tw_fft_sub, NoNeed{}, LdsIO<FS>{lds}, LdsPsi<F>{lds, a.tw_dmap});
+                lds_transform<F, false, LOGN, LdsIO<F>, Reveal, NoNeed, BigSub<LOGN>::FEND, 32, NT>(
+                    lds, a.mtrunc, a.tw_fft, NoNeed{}, LdsIO<F>{lds}, rv);
+            } else {
+                lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NoNeed, 1, 32, NT>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
+            }
         }
         return;
     }
@@ -1383,29 +1438,6 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
 // chunk's first IFFT pass reads its rows from HBM, its last XORs the results
 // into acc (chunk 0: writes acc), and the FFT's last pass writes the parity
 // rows (or compares them, verify).
-// (lo, hi) <-> (lo ^ D(hi), hi) on every symbol of v (t: make_sub_dmap table).
-template <class F>
-__device__ __forceinline__ void sub_swap(typename F::Vec &v, const uint32_t *__restrict__ t) {
-#pragma unroll
-    for (int i = 0; i < F::W; i++) {
-        const uint32_t h = v.h[i];
-        v.l[i] = xor3(v.l[i] ^ perm(t[1], t[0], h & 0x07070707u), perm(t[3], t[2], (h >> 3) & 0x07070707u),
-                      perm(t[4], t[4], (h >> 6) & 0x03030303u));
-    }
-}
-
-// LDS sink that changes rows into subfield coordinates on their way in.
-template <class F>
-struct LdsPsi {
-    uint8_t *lds;
-    const uint32_t *dmap;
-    __device__ void operator()(int row, int u, const typename F::Vec &v0) const {
-        typename F::Vec v = v0;
-        sub_swap<F>(v, dmap);
-        LTile<F>::put(lds, row, u, v);
-    }
-};
-
 // FT: the field of the final FFT (F16S: subfield coordinates, EncodeArgs::tw_fft_sub).
 // ISUB: the chunk IFFTs' subfield passes (EncodeArgs::tw_ifft_sub; needs FT = F16S).
 template <class F, int LOGM, bool VERIFY, class FT = F, bool ISUB = false>
@@ -1540,18 +1572,24 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
     }
 }
 
-template <class F, class FT, int LOGN>
-hipError_t rec_lds_t(const RecArgs &a, hipStream_t s) {
+template <class F, class FT, int LOGN, bool BSUB>
+hipError_t rec_lds_tb(const RecArgs &a, hipStream_t s) {
     const unsigned gx = (unsigned)((a.S + LTile<F>::TB - 1) / LTile<F>::TB);
     if (!a.base || a.nstripes <= 1) {
-        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), dim3(gx), dim3(rec_lds_threads<LOGN>()), 0, s, a);
+        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN, BSUB>), dim3(gx), dim3(rec_lds_threads<LOGN>()), 0, s, a);
         return hipGetLastError();
     }
     return for_y(a.nstripes, [&](int y0, int ny) {  // batched strided stripes: grid.y = stripe
         RecArgs b = a;
         b.base = a.base + (uint64_t)y0 * a.stripe_stride;
-        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN>), dim3(gx, (unsigned)ny), dim3(rec_lds_threads<LOGN>()), 0, s, b);
+        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN, BSUB>), dim3(gx, (unsigned)ny), dim3(rec_lds_threads<LOGN>()), 0, s, b);
     });
+}
+template <class F, class FT, int LOGN>
+hipError_t rec_lds_t(const RecArgs &a, hipStream_t s) {
+    if constexpr (LOGN > 8)
+        if (a.tw_ifft_sub && a.tw_fft_sub && a.tw_dmap) return rec_lds_tb<F, FT, LOGN, true>(a, s);
+    return rec_lds_tb<F, FT, LOGN, false>(a, s);
 }
 template <class F, class FT = F>
 hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {

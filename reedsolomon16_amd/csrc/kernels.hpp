@@ -111,6 +111,10 @@ struct RecArgs {
     // words and each work row's output index (-1: not revealed), both in HBM
     const uint32_t *need_w;
     const int *rev;
+    // n = 512 .. 2048, optional: subfield tables (kTwDwords8, zero where a slot
+    // is full-field) of the passes kernels.hip BigSub<logn> runs in subfield
+    // coordinates, and the coordinate-change map; nullptr: full field throughout
+    const uint32_t *tw_ifft_sub, *tw_fft_sub, *tw_dmap;
 };
 // sub: GF(2^16) transforms in subfield coordinates (tw_ifft/tw_fft are
 // kTwDwords8 subfield tables; tw_in/tw_out fold in the coordinate change).
