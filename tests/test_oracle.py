@@ -195,9 +195,9 @@ def test_simd_port_matches_scalar_oracle(k, p, S, threads, isa):
 
 def test_c5_chunk_twiddles_are_chunk0_plus_layer_constant():
     """The structure behind a bit-sliced m = 256 encode:
-    FFTInitialize builds fftSkew[j + 2^(i+1)] = fftSkew[j] ^ temp[i]
-    (leopard16.go:877-900), so the twiddles of chunk c's ifftDITEncoder
-    (skew offset (c+1)*m - 1, leopard16.go:153-171) are chunk 0's XOR a
+    initFFTSkew builds fftSkew[j + 2^(i+1)] = fftSkew[j] ^ temp[i]
+    (leopard16.go:986-1031), so the twiddles of chunk c's ifftDITEncoder
+    (skewLUT advanced by m per chunk, leopard16.go:176-207) are chunk 0's XOR a
     constant per layer: 8 distinct differences per chunk at m = 256, i.e.
     one full-field constant network per (layer, chunk) on top of networks
     shared by every chunk."""
@@ -211,3 +211,48 @@ def test_c5_chunk_twiddles_are_chunk0_plus_layer_constant():
         for L in range(8):
             assert len(set(d[layer == L].tolist())) == 1, (c, L)
         assert len(set(d.tolist())) == 8
+
+
+def _is_sub(F, lg):
+    return lg == F.mod or int(F.exp[lg]) < 256
+
+
+def test_c5_chunk_subfield_passes():
+    """What k_enc_lds's subfield chunk passes rely on (codec.cpp
+    upload_ifft_sub): at m = 256 chunk c's IFFT twiddles
+    fftSkew[(c+1) 256 - 1 + g 2^(L+1) + 2^L] (ifftDITEncoder leopard16.go:699-741)
+    are full-field only in layers 0 (c = 0), 0-1 (c = 1, 2) and 0-2 (c = 3),
+    so the first all-subfield radix-4 pass (layer pairs 0-1, 2-3, ...) is 1,
+    1, 1, 2."""
+    from oracle import leopard_np as lnp
+
+    F = lnp.field(16)
+    full = {}
+    for c in range(4):
+        full[c] = sorted({L for L in range(8) for g in range(128 >> L)
+                          if not _is_sub(F, int(F._skew[(c + 1) * 256 - 1 + g * (2 << L) + (1 << L)]))})
+    assert full == {0: [0], 1: [0, 1], 2: [0, 1], 3: [0, 1, 2]}
+    assert [max(f) // 2 + 1 for f in full.values()] == [1, 1, 1, 2]
+
+
+def test_big_n_decoder_subfield_layers():
+    """What k_rec_lds's BigSub passes rely on (kernels.hip BigSub, codec.cpp
+    upload_big_sub): the decoder twiddle of layer L, rows (a, a + 2^L) is
+    fftSkew[(a & ~(2^(L+1) - 1)) + 2^L - 1] (ifftDITDecoder / fftDIT,
+    leopard16.go:573-657); at n = 512, 1024, 2048 it is full-field only in
+    layers 0, 0-1, 0-2, so the IFFT is subfield from radix-4 pass 1 (pass 2 at
+    n = 2048) on and the FFT (passes from the top layer down) for its first
+    four passes."""
+    from oracle import leopard_np as lnp
+
+    F = lnp.field(16)
+    for logn, want in ((9, [0]), (10, [0, 1]), (11, [0, 1, 2])):
+        n = 1 << logn
+        full = sorted({L for L in range(logn) for g in range(n >> (L + 1))
+                       if not _is_sub(F, int(F._skew[g * (2 << L) + (1 << L) - 1]))})
+        assert full == want, logn
+        ni = max(full) // 2 + 1
+        assert ni == (2 if logn == 11 else 1)
+        # FFT radix-4 passes cover layers (logn-1, logn-2), (logn-3, logn-4), ...:
+        # the first four never reach a full-field layer
+        assert logn - 8 > max(full)
