@@ -1508,13 +1508,12 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
                 // full-field passes, the last one writing subfield coordinates, then subfield passes
                 const LdsPsi<F> psi{cur, a.tw_dmap};
                 const LdsIO<FT> lios{cur};
-                if (a.ifft_nff[c] == 1) {
-                    lds_transform<F, true, LOGM, ChunkIn, LdsPsi<F>, NoNeed, 0, 1, 256, true>(cur, cnt, tw, NoNeed{}, in, psi);
-                    lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 1, NP - 1>(cur, cnt, tws, NoNeed{}, lios, lios);
-                } else {
-                    lds_transform<F, true, LOGM, ChunkIn, LdsPsi<F>, NoNeed, 0, 2, 256, true>(cur, cnt, tw, NoNeed{}, in, psi);
-                    lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 2, NP - 1>(cur, cnt, tws, NoNeed{}, lios, lios);
-                }
+                const int nff = a.ifft_nff[c];  // 1 or 2 (codec.cpp upload_ifft_sub)
+                if (nff == 1) lds_transform<F, true, LOGM, ChunkIn, LdsPsi<F>, NoNeed, 0, 1, 256, true>(cur, cnt, tw, NoNeed{}, in, psi);
+                else lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, 1>(cur, cnt, tw, NoNeed{}, in, lio);
+                if (nff == 2) lds_transform<F, true, LOGM, LdsIO<F>, LdsPsi<F>, NoNeed, 1, 2, 256, true>(cur, cnt, tw, NoNeed{}, lio, psi);
+                else lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 1, 2>(cur, cnt, tws, NoNeed{}, lios, lios);
+                lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 2, NP - 1>(cur, cnt, tws, NoNeed{}, lios, lios);
             } else {
                 lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, NP - 1>(cur, cnt, tw, NoNeed{}, in, lio);
             }

@@ -404,10 +404,12 @@ def test_host_pipeline_c3_pinned_matches_device(torch_dev):
     assert c.verify(shards)
 
 
-@pytest.mark.parametrize("k,p", [(128, 32), (100, 28), (10, 4)])
+@pytest.mark.parametrize("k,p", [(128, 32), (100, 28), (10, 4), (300, 100), (700, 200), (1024, 256)])
 def test_reconstruct_subfield_equals_full_field(torch_dev, monkeypatch, k, p):
-    """The LDS reconstruct in GF(2^8)-subfield coordinates (default for n <= 256)
-    and the full-field table path (RS_NO_SUB=1) rebuild identical bytes."""
+    """The LDS reconstruct in GF(2^8)-subfield coordinates (every pass for
+    n <= 256, all but the first passes of each transform at n = 512..2048:
+    kernels.hip BigSub) and the full-field table path (RS_NO_SUB=1) rebuild
+    identical bytes."""
     torch = torch_dev
     S = 4096 + 192
     g = torch.Generator(device="cuda")
@@ -964,3 +966,27 @@ def test_verify_and_reconstruct_async_stream_of_blocks(k, p, S):
         c.verify_async(list(blocks[0])).wait()
     with pytest.raises(rs.codec.RSError):
         rs.codec.VerifyTicket(c, old, None).result()
+
+
+@pytest.mark.parametrize("k,p,S", [(1024, 256, 1024), (300, 200, 512), (100, 40, 256), (1000, 129, 128)])
+def test_lds_encode_subfield_chunk_passes(torch_dev, monkeypatch, k, p, S):
+    """k_enc_lds with the chunk IFFTs in subfield coordinates from their first
+    all-subfield pass on (EncodeArgs::tw_ifft_sub, default) and the full-field
+    chunk IFFTs (RS_NO_SUB=1) both give the oracle's parity, and verify it."""
+    torch = torch_dev
+    rng = np.random.default_rng(k + p + S)
+    data = rand_data(rng, k, S)
+    ref = orc.encode(16, k, p, data)
+    for nosub in ("0", "1"):
+        monkeypatch.setenv("RS_NO_SUB", nosub)
+        c = rs.New16(k, p)
+        assert c.encode_path.startswith("lds-m")
+        slab = torch.zeros((2, k + p, S), dtype=torch.uint8, device="cuda")
+        slab[:, :k] = torch.from_numpy(data).cuda()
+        c.encode_dev_batch(slab)
+        torch.cuda.synchronize()
+        for z in range(2):
+            assert np.array_equal(slab[z, k:].cpu().numpy(), ref), (nosub, z)
+        assert c.verify_dev_batch(slab)
+        slab[1, k + p - 1, 3] ^= 0x40
+        assert not c.verify_dev_batch(slab)
