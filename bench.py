@@ -29,7 +29,7 @@ achieved = algorithmic bytes per launch ((k+p)*bytes-per-row: read k rows,
 write p rows) / its mean duration (one HIP event pair on the launch stream
 around the timed launches, divided by their count).  `single_stripe` repeats
 the kernel timing with one stripe per launch (the reference's Encode
-granularity).  Resident rows sit at a stride of row bytes + --row-pad (3 KiB
+granularity).  Resident rows sit at a stride of row bytes + --row-pad (3.5 KiB
 by default); `unpadded_rows` times the same launch on rows
 packed exactly one row length apart.  `other_workloads` (one GPU) reports the
 kernel time and roofline fraction of the C4 reconstruct and the C5 encode
@@ -259,7 +259,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="skip the one-stripe-per-launch figure")
-    ap.add_argument("--row-pad", type=int, default=3072,
+    ap.add_argument("--row-pad", type=int, default=3584,
                     help="bytes between consecutive resident rows (HBM layout: row stride = row bytes + pad; "
                          "64-byte multiple); the unpadded layout is timed too and reported beside it")
     ap.add_argument("--no-unpadded", action="store_true", help="skip timing the unpadded layout")
@@ -311,7 +311,8 @@ def main():
     # this rank's resident bytes: B stripes x (k+p) rows x W bytes (its byte
     # range), rows at a stride of W + row_pad bytes (rows exactly
     # a power of two apart put every row's column tile on the same low address
-    # bits; a 3 KiB stagger measured 5-6 % faster at C3).  `flat` is the same
+    # bits; a 3.5 KiB stagger measured the fastest of 27 at C3, 3.4 % over 3 KiB,
+    # profiles/r04_row_pad_sweep.txt).  `flat` is the same
     # memory as an unpadded [B, k+p, W] slab, timed for comparison.
     pad = args.row_pad
     if pad % 64:
