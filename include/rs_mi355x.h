@@ -150,6 +150,18 @@ int rs_join(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nsh
  * per segment.  Segment width per row: `bytes` (multiple of 64) or 0 for
  * automatic (about 8 MiB copied in per segment). */
 int rs_set_host_segment(rs_codec *codec, size_t bytes);
+
+/* GF(2^8) reconstruct with the reference's inversion cache semantics
+ * (leopard8.go:508-555, codecs of at most 64 shards: :67-71).  The reference
+ * looks its cached errLocs up by the raw erasure bitfield, which leaves out
+ * parity erasures unless recoverAll, and stores them under the bitfield after
+ * prepare(); a later call whose erasures differ only in ways the key does not
+ * see then reuses errLocs computed for another pattern, and rebuilds wrong
+ * data.  By default (on = 0) the engine keys its caches on the exact pattern
+ * and always rebuilds the right data; on = 1 reproduces the reference's output
+ * call for call, stale results included.  Switching clears the cache, as a
+ * fresh newFF8 would.  No effect on GF(2^16) codecs or above 64 shards. */
+int rs_set_reference_inversion_cache(rs_codec *codec, int on);
 /* Pinned, 64-byte-aligned host memory: AllocAligned (unsafe.go:17-41) for
  * shards that are to cross PCIe at full rate. */
 int rs_host_alloc(size_t bytes, void **out);

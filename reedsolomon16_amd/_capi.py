@@ -49,6 +49,7 @@ def lib() -> C.CDLL:
     L.rs_verify_dev_batch.argtypes = [vp, vp, sz, sz, i32, sz, P(i32), vp]
     L.rs_encode_dev_batch.argtypes = [vp, vp, sz, sz, i32, sz, vp]
     L.rs_set_host_segment.argtypes = [vp, sz]
+    L.rs_set_reference_inversion_cache.argtypes = [vp, i32]
     L.rs_split_shard_size.argtypes = [vp, sz, P(sz)]
     L.rs_split.argtypes = [vp, vp, sz, vp, sz, vp]
     L.rs_join.argtypes = [vp, P(vp), P(sz), i32, vp, sz, vp]

@@ -257,6 +257,13 @@ class ReedSolomon:
         """Column-segment width of the host pipeline (0 = automatic)."""
         _check(self._L.rs_set_host_segment(self._h, nbytes))
 
+    def set_reference_inversion_cache(self, on: bool) -> None:
+        """GF(2^8): reproduce leopard8.go:508-555's inversion cache call for
+        call, including the stale errLocs it hands out when two erasure
+        patterns share its key (include/rs_mi355x.h).  Off by default: the
+        engine keys its caches on the exact pattern."""
+        _check(self._L.rs_set_reference_inversion_cache(self._h, 1 if on else 0))
+
     # ---------------- host-memory operations (Go [][]byte semantics)
     def encode(self, shards: list) -> None:
         """Encode (leopard16.go:116-125): parity written into shards[k:]."""

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cstring>
 #include <list>
@@ -205,6 +206,12 @@ struct rs_codec {
 
     // error-locator cache keyed by erasure pattern (bounded LRU)
     std::list<std::pair<std::vector<uint8_t>, std::vector<uint32_t>>> el_cache;
+    // rs_set_reference_inversion_cache: the GF(2^8) inversion cache exactly as
+    // leopard8.go:508-555 keys it (raw erasure bits on lookup, bits after
+    // prepare() on store), for callers that need the reference's output on
+    // every call sequence; off by default
+    bool ref_inv = false;
+    std::map<std::array<uint64_t, 4>, std::vector<uint32_t>> ref_inv_cache;
 
     // host-resident pipeline (rs_encode / rs_verify / rs_reconstruct): copy-in,
     // compute and copy-out streams over kHostBufs rotating staging slabs
@@ -693,13 +700,65 @@ const std::vector<uint32_t> *error_locs_cached(rs_codec *c, const std::vector<ui
 }
 
 
-int plan_reconstruct_new(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, RecPlan &pl);
+// The reference-keyed GF(2^8) inversion cache (rs_set_reference_inversion_cache).
+// leopard8.go:481-506 builds the error bitfield: parity erasures (and the
+// padding rows p..m-1) only when recoverAll, data erasure i at bit i + m; the
+// lookup (:509-524) uses those raw bits, a miss stores its errLocs (:542-554)
+// under the bits after prepare() when useBits (:474), whose first level pairs
+// bits 2i and 2i+1 (:1192-1199).  A hit hands back errLocs computed for
+// whatever pattern stored them, which is the reference's output on that call.
+// Pruning from a hit's stored bits covers every row the call rebuilds, so
+// only errLocs decides the result.  Returns nullptr when the mode is off or
+// the reference keeps no cache for this codec (GF(2^16), or total > 64: :67-71).
+const std::vector<uint32_t> *ref_inv_errlocs(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
+                                             uint64_t S) {
+    if (!c->ref_inv || c->bits != 8 || c->total > 64) return nullptr;
+    const int k = c->k, p = c->p, m = c->m, total = c->total;
+    std::array<uint64_t, 4> w{};
+    auto set = [&](int b) { w[b >> 6] |= 1ull << (b & 63); };
+    int npresent = 0;
+    for (int i = 0; i < total; i++) npresent += present[i] ? 1 : 0;
+    for (int i = 0; i < p; i++)
+        if (!present[k + i] && recover_all) set(i);
+    for (int i = p; i < m; i++)
+        if (recover_all) set(i);
+    for (int i = 0; i < k; i++)
+        if (!present[i]) set(i + m);
+    auto it = c->ref_inv_cache.find(w);
+    if (it != c->ref_inv_cache.end()) return &it->second;
+    std::vector<uint8_t> erased(total);
+    for (int i = 0; i < total; i++) erased[i] = !present[i];
+    std::vector<uint32_t> el;
+    if (!error_locators(*c->F, k, p, erased.data(), el)) return nullptr;
+    const bool use_bits = total - npresent <= p / 4 && S * (uint64_t)total >= (64u << 10);
+    if (use_bits)
+        for (uint64_t &x : w) x |= ((x & 0xAAAAAAAAAAAAAAAAull) >> 1) | ((x & 0x5555555555555555ull) << 1);
+    auto &slot = c->ref_inv_cache[w];
+    slot = std::move(el);
+    return &slot;
+}
+
+int plan_reconstruct_new(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
+                         const std::vector<uint32_t> *el_ref, RecPlan &pl);
+
+// Plan-cache key: (erasure pattern, recover_all), plus the errLocs a
+// reference-keyed cache handed out, which can differ between calls with the
+// same pattern.
+std::vector<uint8_t> plan_key(const std::vector<uint8_t> &present, bool recover_all, const std::vector<uint32_t> *el_ref) {
+    std::vector<uint8_t> key(present);
+    key.push_back(recover_all ? 1 : 0);
+    if (el_ref) {
+        const uint8_t *b = (const uint8_t *)el_ref->data();
+        key.insert(key.end(), b, b + el_ref->size() * sizeof(uint32_t));
+    }
+    return key;
+}
 
 // Plans are cached per (erasure pattern, recover_all): repeated repairs of
 // the same pattern skip the table construction.
-int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, RecPlan &pl) {
-    std::vector<uint8_t> key(present);
-    key.push_back(recover_all ? 1 : 0);
+int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, uint64_t S, RecPlan &pl) {
+    const std::vector<uint32_t> *el_ref = ref_inv_errlocs(c, present, recover_all, S);
+    std::vector<uint8_t> key = plan_key(present, recover_all, el_ref);
     for (auto it = c->plan_cache.begin(); it != c->plan_cache.end(); ++it) {
         if (it->first == key) {
             c->plan_cache.splice(c->plan_cache.begin(), c->plan_cache, it);
@@ -707,21 +766,22 @@ int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool reco
             return RS_OK;
         }
     }
-    int e = plan_reconstruct_new(c, present, recover_all, pl);
+    int e = plan_reconstruct_new(c, present, recover_all, el_ref, pl);
     if (e) return e;
     c->plan_cache.emplace_front(std::move(key), pl);
     if (c->plan_cache.size() > 16) c->plan_cache.pop_back();
     return RS_OK;
 }
 
-int plan_reconstruct_new(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, RecPlan &pl) {
+int plan_reconstruct_new(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
+                         const std::vector<uint32_t> *el_ref, RecPlan &pl) {
     int e = build_decode_plan(c);
     if (e) return e;
     if (!c->dec_ok) return RS_ERR_PANIC;
     const int k = c->k, p = c->p, m = c->m, n = c->n, total = c->total;
     std::vector<uint8_t> erased(total);
     for (int i = 0; i < total; i++) erased[i] = !present[i];
-    const std::vector<uint32_t> *elp = error_locs_cached(c, erased);
+    const std::vector<uint32_t> *elp = el_ref ? el_ref : error_locs_cached(c, erased);
     if (!elp) return RS_ERR_PANIC;
     const std::vector<uint32_t> &el = *elp;
     // work rows: [recovery m][original k][zero to n] (leopard16.go:547)
@@ -840,9 +900,8 @@ void set_big_sub(const rs_codec *c, RecArgs &ra) {
 }
 
 // Device-resident plan for (present, recover_all), built and uploaded on first use.
-int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, DevPlan **out) {
-    std::vector<uint8_t> key(present);
-    key.push_back(recover_all ? 1 : 0);
+int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, uint64_t S, DevPlan **out) {
+    std::vector<uint8_t> key = plan_key(present, recover_all, ref_inv_errlocs(c, present, recover_all, S));
     for (auto it = c->dplan_cache.begin(); it != c->dplan_cache.end(); ++it) {
         if (it->first == key) {
             c->dplan_cache.splice(c->dplan_cache.begin(), c->dplan_cache, it);
@@ -851,7 +910,7 @@ int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
         }
     }
     auto dp = std::make_unique<DevPlan>();
-    if (int e = plan_reconstruct(c, present, recover_all, dp->pl)) return e;
+    if (int e = plan_reconstruct(c, present, recover_all, S, dp->pl)) return e;
     const RecPlan &pl = dp->pl;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t s_in = pl.tw_in.size() * 4, s_out = pl.tw_out.size() * 4, s_pos = std::max<size_t>(pl.pos.size(), 1) * 4;
@@ -932,7 +991,7 @@ int launch_rec_plan(rs_codec *c, DevPlan *dpl, uint8_t *base, uint64_t stride, u
 int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uint8_t> &present, uint64_t S,
                            bool recover_all, hipStream_t s) {
     DevPlan *dp = nullptr;
-    if (int e = dev_plan(c, present, recover_all, &dp)) return e;
+    if (int e = dev_plan(c, present, recover_all, S, &dp)) return e;
     const RecPlan &pl = dp->pl;
     const int n = c->n, nd = (int)pl.dst_shard.size();
     if (!nd) return RS_OK;
@@ -1011,7 +1070,7 @@ int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uin
 int reconstruct_device(rs_codec *c, uint8_t *const *d, const std::vector<uint8_t> &present, uint64_t S,
                        bool recover_all, hipStream_t s) {
     RecPlan pl;
-    int e = plan_reconstruct(c, present, recover_all, pl);
+    int e = plan_reconstruct(c, present, recover_all, S, pl);
     if (e) return e;
     e = scratch_acquire(c, s);
     if (e) return e;
@@ -1192,11 +1251,11 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     if (op == HostOp::Reconstruct) {
         if (int be = build_decode_plan(c)) return be;
         if (c->dec_ok && rec_lds_ok(c)) {
-            e = dev_plan(c, present, recover_all, &dpl);
+            e = dev_plan(c, present, recover_all, S, &dpl);
             if (e) return e;
             pl = dpl->pl;
         } else {
-            e = plan_reconstruct(c, present, recover_all, pl);
+            e = plan_reconstruct(c, present, recover_all, S, pl);
             if (e) return e;
         }
         for (int i = 0; i < total; i++)
@@ -1659,7 +1718,7 @@ int rs_reconstruct_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size
     if (c->dec_ok && rec_lds_ok(c)) {
         // one launch: grid.y = stripe, the pattern's tables shared (dev_plan cache)
         DevPlan *dpl = nullptr;
-        if (int e = dev_plan(c, pr, recover_all != 0, &dpl)) return e;
+        if (int e = dev_plan(c, pr, recover_all != 0, S, &dpl)) return e;
         if (int e = launch_rec_plan(c, dpl, base, row_stride, stripe_stride, (int)nstripes, S, s)) return e;
         if (!stream) HIP_TRY(hipStreamSynchronize(s));  // no caller stream: complete on return
         return RS_OK;
@@ -1965,6 +2024,14 @@ int rs_set_host_segment(rs_codec *c, size_t bytes) {
     if (!c || bytes % 64) return RS_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     c->host_seg_bytes = bytes;
+    return RS_OK;
+}
+
+int rs_set_reference_inversion_cache(rs_codec *c, int on) {
+    if (!c) return RS_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->ref_inv = on != 0;
+    c->ref_inv_cache.clear();
     return RS_OK;
 }
 

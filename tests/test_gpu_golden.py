@@ -15,7 +15,9 @@
   error-locator vector reused for a different parity-erasure pattern): the
   engine keys its cache on the exact pattern and returns the correct shard,
   where the reference (oracle) returns the stale result.  INTEGRATION.md
-  states this divergence.
+  states this divergence; rs_set_reference_inversion_cache(1) reproduces the
+  reference's results call for call (random call sequences, host and device
+  entry points, against the oracle).
 """
 import os
 
@@ -148,6 +150,71 @@ def test_gf8_inversion_cache_sequence():
     sh = [None if i == 0 else full[i].copy() for i in range(k + p)]
     c.reconstruct_data(sh)
     assert np.array_equal(sh[0], full[0])  # the engine's (correct) result
+
+
+def test_gf8_inversion_cache_sequence_reference_mode():
+    """rs_set_reference_inversion_cache(1): the same sequence returns the
+    reference's stale shard 0, byte for byte the oracle's."""
+    k, p, S = 10, 4, 64
+    data = np.random.default_rng(2).integers(0, 256, (k, S), dtype=np.uint8)
+    par = orc.encode(8, k, p, data)
+    full = [data[i] for i in range(k)] + [par[i] for i in range(p)]
+    o = orc.Oracle(8, k, p)
+    c = rs.New8(k, p)
+    c.set_reference_inversion_cache(True)
+    for erased in ((0, k), (0,)):
+        e, ref = o.reconstruct([None if i in erased else full[i].copy() for i in range(k + p)], False)
+        assert e == 0
+        sh = [None if i in erased else full[i].copy() for i in range(k + p)]
+        c.reconstruct_data(sh)
+        assert np.array_equal(sh[0], ref[0])
+    assert not np.array_equal(sh[0], full[0])  # the stale result, as the reference returns it
+
+
+@pytest.mark.parametrize("entry", ["host", "device"])
+@pytest.mark.parametrize("S", [64, 2048])
+def test_gf8_reference_inversion_cache_random_sequences(torch, entry, S):
+    """60 reconstructs of one GF(2^8) codec (40 + 16: total <= 64, so the
+    reference caches) over erasure sets drawn from a few shards, with random
+    recoverAll, in reference mode: every rebuilt shard equals the oracle's on
+    the same call sequence.  At S = 2048 one-to-four erasures take the
+    reference's useBits branch (leopard8.go:474), whose store key is the
+    prepared bitfield (:1192-1199), so a later pattern with both bits of a
+    pair erased reuses errLocs computed for one of them; at S = 64 only the
+    parity bits left out of the key collide.  Both kinds of stale hit occur."""
+    k, p = 40, 16
+    rng = np.random.default_rng(S + (1 if entry == "device" else 0))
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    par = orc.encode(8, k, p, data)
+    full = np.concatenate([data, par])
+    o = orc.Oracle(8, k, p)
+    c = rs.New8(k, p)
+    c.set_reference_inversion_cache(True)
+    pool = [0, 1, 2, 3, 6, 7, k, k + 1, k + 5]
+    stale = 0
+    for _ in range(60):
+        er = sorted(set(int(x) for x in rng.choice(pool, int(rng.integers(1, 5)), replace=False)))
+        ra = bool(rng.integers(0, 2))
+        e, ref = o.reconstruct([None if i in er else full[i].copy() for i in range(k + p)], ra)
+        assert e == 0
+        if entry == "host":
+            sh = [None if i in er else full[i].copy() for i in range(k + p)]
+            (c.reconstruct if ra else c.reconstruct_data)(sh)
+            got = sh
+        else:
+            present = np.ones(k + p, bool)
+            present[er] = False
+            slab = torch.from_numpy(full.copy()).cuda()
+            slab[torch.tensor(er).cuda()] = 0
+            c.reconstruct_dev(slab, present, recover_all=ra)
+            torch.cuda.synchronize()
+            got = slab.cpu().numpy()
+        for i in er:
+            if ref[i] is None:
+                continue
+            assert np.array_equal(got[i], ref[i]), (er, ra, i)
+            stale += not np.array_equal(ref[i], full[i])
+    assert stale > 0  # the sequence exercised the reference's stale hits
 
 
 @pytest.mark.parametrize("bits,k,p", [(16, 128, 32), (8, 128, 32), (16, 100, 28), (8, 10, 4)])
