@@ -2,13 +2,14 @@
 128 data + 32 parity x 1 MiB shards (configs[2] / C3) by default, or
 1024 + 256 x 256 KiB (configs[4] / C5) with --workload C5.
 
-A step encodes B synthetic stripes (--stripes, default 128: 20 GiB of C3
+A step encodes B synthetic stripes (--stripes, default 256: 40 GiB of C3
 stripes resident, a small fraction of the 288 GB HBM) already resident in HBM,
 in one kernel launch per rank (rs_encode_dev_batch).  Larger batches amortise
-the persistent grid's fill and drain: on one box the 8-rank byte-range slice
-(128 KiB of every row) ran at 0.58-0.59 / 0.62 / 0.61-0.64 of the HBM
-roofline for 64 / 128 / 256 stripes per launch, full rows at 0.61 / 0.61-0.62
-/ 0.63-0.64 for 32 / 128 / 256 (profiles/r02_batch_slice.txt).
+the grid's fill and drain, which weighs most on the small per-rank slices of
+a byte-range split: on one box the 8-rank slice (128 KiB of every row) ran at
+0.608 / 0.624 / 0.627 of the HBM roofline for 128 / 256 / 512 stripes per
+launch, the 2-rank slice at 0.640 for 128 and 256, full rows at 0.652 / 0.650
+for 128 / 256 (profiles/r04_batch_slices.txt).
 
 Multi-GPU (one process per GPU).  Under torch.distributed.run (WORLD_SIZE set)
 every rank checks WORLD_SIZE == --gpus.  Started directly with --gpus N > 1,
@@ -254,7 +255,7 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="C3")
     ap.add_argument("--split", choices=["bytes", "stripes"], default="bytes",
                     help="multi-GPU layout: byte ranges of the same stripes (strong) or own stripes (weak)")
-    ap.add_argument("--stripes", type=int, default=128, help="stripes encoded per step (one launch per rank)")
+    ap.add_argument("--stripes", type=int, default=256, help="stripes encoded per step (one launch per rank)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
     ap.add_argument("--no-cpu", action="store_true")
