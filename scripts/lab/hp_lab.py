@@ -37,4 +37,24 @@ rep("                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, v
     "                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, soff, 0);")
 rep("                            __builtin_amdgcn_raw_buffer_store_b128(v, ps, voff + k * QS, soff, 0);",
     "                            __builtin_amdgcn_raw_buffer_store_b128(v, ps, (RS_HP_ABL & 16) ? voff - (uint32_t)blk * 48 + (uint32_t)k * 512 : voff + k * QS, soff, 0);")
+# 32 / 64: PF1 = 1 / 3 rows of the next chunk before phase 1 (m = 32)
+rep("    static constexpr int PF1 = LOGM == 5 ? 2 : HR / 2;",
+    "    static constexpr int PF1 = LOGM == 5 ? ((RS_HP_ABL & 32) ? 1 : (RS_HP_ABL & 64) ? 3 : 2) : HR / 2;")
+# 128: the first prefetch part right after the staged rows are copied, before the transposes
+rep("""        for (int i = 0; i < HR; i++) {
+            abl_t8(R[i]);""", """        for (int i = 0; i < HR; i++) {
+            if constexpr (RS_HP_ABL & 128) if (i == 0) {
+                _Pragma("unroll") for (int i2 = 0; i2 < RW; i2++) _Pragma("unroll") for (int q = 0; q < 8; q++) asm volatile("" : "+v"(R[i2][q])::"memory");
+                __builtin_amdgcn_sched_barrier(0);
+                prefetch<C, 0, PF1>(cur, nxt);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            abl_t8(R[i]);""")
+rep("""        __builtin_amdgcn_sched_barrier(0);
+        prefetch<C, 0, PF1>(cur, nxt);
+        __builtin_amdgcn_sched_barrier(0);
+        dispatch<4>""", """        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(RS_HP_ABL & 128)) prefetch<C, 0, PF1>(cur, nxt);
+        __builtin_amdgcn_sched_barrier(0);
+        dispatch<4>""")
 open(p, "w").write(s)
