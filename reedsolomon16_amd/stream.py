@@ -1,7 +1,13 @@
-"""Pipelined mirror of the reference's GF(2^16) stream codec ``rsStream16``
-(bpfs/reedsolomon16 streaming16.go:16-71, 200-632, 1229-1318), with its
+"""Pipelined mirrors of the reference's stream codecs, with their
 ``r.rs.Encode / Verify / Reconstruct / ReconstructData`` calls bound to the
-MI355X engine's asynchronous tickets.
+MI355X engine's asynchronous tickets:
+
+* ``StreamEncoder16`` -- ``rsStream16`` (bpfs/reedsolomon16
+  streaming16.go:16-71, 84-632, 1229-1318), the GF(2^16) stream codec that
+  ``New16`` hands out;
+* ``StreamEncoder8`` -- ``rsStreamFF8`` (streaming8.go:50-101, 109-181,
+  242-340, 343-766), the GF(2^8) stream codec behind ``New`` for every
+  k + p <= 256 (reedsolomon.go:77-80, 124-202).
 
 This is the edit INTEGRATION.md describes for the Go side: the reference reads
 one 4 MiB block per shard, calls the codec, writes the block out, and only then
@@ -13,16 +19,37 @@ Block semantics follow the Go loops byte for byte (they decide which bytes the
 codec sees, so parity and verdicts match the reference's for the same readers):
 
 * the block size is the first non-empty shard's read (``readInputs``
-  streaming16.go:84-170); other shards are zero-extended or truncated to it;
-* encode pads the block to an even size and then to a multiple of 64 with
-  zeros and writes ``ceil64(size)`` parity bytes (:1274-1318, :173-197);
-* verify pads to even with zeros, then to 64 *without* zero-filling: its fill
-  loop starts at ``len(all[i])`` after the reslice (:304-306), so those bytes
-  are whatever the single Go block buffer last held there.  The mirror
-  reproduces that content (``_GoBufferHistory``);
-* reconstruct zero-pads present shards to 64 and writes ``origSize`` bytes of
-  rebuilt data shards and ``ceil64(size)`` of rebuilt parity (:320-468);
-  reconstructData (:471-632) feeds a nil parity input as a zero shard.
+  streaming16.go:84-170, streaming8.go:242-316); other shards are
+  zero-extended or truncated to it;
+* encode pads the block with zeros -- to an even size first in GF(2^16) --
+  then to a multiple of 64, and writes ``ceil64(size)`` parity bytes
+  (streaming16.go:1274-1318, :173-197; streaming8.go:155-181, :318-340);
+* verify zero-pads the same way (streaming16.go:245-309, streaming8.go:388-436).
+  In GF(2^16) every row reaching :295 is exactly ``size`` bytes long, so each
+  one is replaced by a fresh zeroed ``make([]byte, alignedSize)`` (:297-299;
+  the reslice at :301 never runs).  The parity rows' real bytes past ``size``
+  are therefore replaced by zeros.  Whether the block still verifies depends
+  on which bytes the pad covers: where every twiddle of the geometry lies in
+  GF(2^8) (e.g. 128 + 32) a parity symbol's high byte depends only on the
+  data's high bytes, so a pad inside the high half (size mod 64 >= 32) holds
+  zero parity and verifies True; a pad reaching into the low half, or a
+  full-field geometry, verifies False.  After a True verdict the loop's next
+  ``all[i][:r.blockSize]`` (:218) slices past the new buffer's capacity
+  (alignedSize < blockSize) and the reference panics; the mirror raises
+  ``ErrPanic`` there.  GF(2^8) keeps the block buffer (capacity blockSize) and
+  never panics; its byte columns are independent, so the zero pad verifies;
+* GF(2^16) reconstruct zero-pads present shards to 64 and writes ``origSize``
+  bytes of rebuilt data shards and ``ceil64(size)`` of rebuilt parity
+  (streaming16.go:320-468); reconstructData (streaming16.go:471-632,
+  streaming8.go:609-766) feeds a nil parity input as a zero shard;
+* GF(2^8) reconstruct (streaming8.go:447-606) has no missing-shard map: its
+  uniform-size loop (:389-393) zero-extends *every* nil input, the missing
+  shards included, so ``r.rs.Reconstruct`` sees every shard present and does
+  nothing (leopard8.go:459-462), and the loop writes zeros for every requested
+  output (``size`` bytes per data shard, ``ceil64(size)`` per parity shard).
+  ``StreamReconstruct`` takes this loop whenever a parity output is requested
+  (reedsolomon.go:174-188); with data outputs only it takes reconstructData,
+  which rebuilds.  The mirror reproduces both.
 
 One observable difference: a pipelined verify reads block j+1 before it learns
 that block j mismatched, so on a ``False`` result the readers have advanced one
@@ -31,13 +58,14 @@ block further than the reference's would have.
 from __future__ import annotations
 
 from collections import deque
-from typing import List, Optional, Sequence
+from typing import Optional, Sequence
 
 import numpy as np
 
-from .codec import EmptyShard, New16, RSError, ErrInvShardNum, ErrShardNoData, ErrTooFewShards
+from .codec import (EmptyShard, New8, New16, RSError, ErrInvShardNum, ErrPanic, ErrShardNoData,
+                    ErrTooFewShards)
 
-BLOCK_SIZE = 4 * 1024 * 1024  # streaming16.go:48
+BLOCK_SIZE = 4 * 1024 * 1024  # streaming16.go:48, streaming8.go:83
 
 
 class ErrReconstructMismatch(RSError):
@@ -94,58 +122,28 @@ def _write(writer, buf: np.ndarray, stream: int) -> None:
         raise StreamWriteError("short write", stream)
 
 
-class _GoBufferHistory:
-    """What the reference's single block buffer holds past a row's current
-    write extent.  Row i's buffer byte x is the byte the latest block that wrote
-    x put there (ReadFull writes [0, n); zero padding writes up to the padded
-    size), or 0 if no block did (AllocAligned zeroes it).  The mirror keeps
-    `depth` buffers, so a byte last written by a block held in another buffer
-    is copied over when a verify block reads it (streaming16.go:290-309)."""
+class _StreamCodec:
+    """The block loops shared by both fields; the subclasses set the field and
+    the places where streaming16.go and streaming8.go differ."""
 
-    def __init__(self, total: int):
-        self.ext: List[List[int]] = [[] for _ in range(total)]  # per row: write extent of each block
-
-    def record(self, extents: Sequence[int]) -> None:
-        for i, e in enumerate(extents):
-            self.ext[i].append(e)
-
-    def fill(self, blk: int, bufs, lo: int, hi: int) -> None:
-        """Give bytes [lo, hi) of every row of block `blk` (already recorded)
-        the reference buffer's content."""
-        depth = len(bufs)
-        cur = bufs[blk % depth]
-        for i, ext in enumerate(self.ext):
-            for x in range(lo, hi):
-                t = blk
-                while t >= 0 and x >= ext[t]:
-                    t -= 1
-                if t < 0:
-                    cur[i][x] = 0
-                elif t % depth != blk % depth:
-                    cur[i][x] = bufs[t % depth][i][x]
-                # else: the byte is still in this buffer from block t
-
-
-class StreamEncoder16:
-    """rsStream16 (streaming16.go:16-71) over the MI355X engine.
-
-    ``encode(inputs, outputs)``, ``verify(shards)``, ``reconstruct(inputs,
-    outputs)`` and ``reconstruct_data(inputs, outputs)`` take file-like readers
-    (``readinto`` or ``read``; None = a nil reader) and writers (``write``;
-    None = nil), like the Go io.Reader / io.Writer slices."""
+    FIELD = 16
+    EVEN = True  # GF(2^16) pads an odd block to even first (streaming16.go:122-125, :274-287)
 
     def __init__(self, data_shards: int, parity_shards: int, device: Optional[int] = None,
                  block_size: int = BLOCK_SIZE, depth: int = 2, codec=None):
-        if data_shards <= 0 or parity_shards <= 0:  # streaming16.go:36-41
+        if data_shards <= 0 or parity_shards <= 0:  # streaming16.go:36-41, streaming8.go:71-76
             raise ErrInvShardNum("invalid number of shards")
-        if block_size % 2:  # streaming16.go:54-56
+        if self.EVEN and block_size % 2:  # streaming16.go:54-56
             block_size += 1
         if block_size % 64 or depth < 1:
             raise ValueError("block_size must be a multiple of 64 and depth >= 1")
-        # newFF16 (streaming16.go:59-63); `codec` substitutes an object with the
-        # same encode_async / verify_async / reconstruct_async / alloc_aligned
-        # methods (the CPU tests drive the block logic with one)
-        self.rs = codec if codec is not None else New16(data_shards, parity_shards, device)
+        # newFF16 / newFF8 (streaming16.go:59-63, streaming8.go:89-93); `codec`
+        # substitutes an object with the same encode_async / verify_async /
+        # reconstruct_async / alloc_aligned methods (the CPU tests drive the
+        # block logic with one)
+        if codec is None:
+            codec = (New16 if self.FIELD == 16 else New8)(data_shards, parity_shards, device)
+        self.rs = codec
         self.k, self.p = data_shards, parity_shards
         self.total = data_shards + parity_shards
         self.block_size = block_size
@@ -153,18 +151,18 @@ class StreamEncoder16:
         self._bufs = None
 
     def _buffers(self):
-        # AllocAligned(totalShards, blockSize) (streaming16.go:66-76), pinned so
-        # the queued copies run as DMA and the tickets return at once
+        # AllocAligned(totalShards, blockSize) (streaming16.go:66-76,
+        # streaming8.go:96-98), pinned so the queued copies run as DMA and the
+        # tickets return at once
         if self._bufs is None:
             self._bufs = [self.rs.alloc_aligned(self.block_size, pinned=True) for _ in range(self.depth)]
         return self._bufs
 
-    # ------------------------------------------------------------------ encode
-    def _read_inputs(self, readers, rows) -> int:
-        """readInputs (streaming16.go:84-170) into `rows` (numpy row views of
-        block_size bytes): returns the (even) block size, -1 at end of stream."""
+    def _read_rows(self, readers, rows, lens) -> int:
+        """The read loop every stream operation opens with: io.ReadFull of up
+        to blockSize bytes per non-nil reader into its row; returns the first
+        non-empty read's length (-1 if none), appends every row's length."""
         size = -1
-        lens = []
         for i, rd in enumerate(readers):
             if rd is None:
                 lens.append(0)
@@ -176,9 +174,18 @@ class StreamEncoder16:
             if n > 0 and size == -1:
                 size = n
             lens.append(n)
+        return size
+
+    # ------------------------------------------------------------------ encode
+    def _read_inputs(self, readers, rows) -> int:
+        """readInputs (streaming16.go:84-170, streaming8.go:242-316) into
+        `rows` (numpy row views of block_size bytes): returns the block size
+        (made even in GF(2^16)), -1 at end of stream."""
+        lens = []
+        size = self._read_rows(readers, rows, lens)
         if size == -1:
             return -1
-        if size % 2:
+        if self.EVEN and size % 2:
             size += 1
         padded = _ceil64(size)
         for i, n in enumerate(lens):
@@ -188,7 +195,8 @@ class StreamEncoder16:
         return size
 
     def encode(self, inputs: Sequence, outputs: Sequence) -> None:
-        """rsStream16.encode (streaming16.go:1229-1318)."""
+        """rsStream16.encode (streaming16.go:1229-1318) / rsStreamFF8.encode
+        (streaming8.go:109-181)."""
         if len(inputs) != self.k or len(outputs) != self.p:
             raise ErrTooFewShards("too few shards given")
         bufs = self._buffers()
@@ -197,7 +205,7 @@ class StreamEncoder16:
         def drain_one():
             t, rows, size = pending.popleft()
             t.wait()
-            al = _ceil64(size)  # writeOutputs (streaming16.go:173-197)
+            al = _ceil64(size)  # writeOutputs (streaming16.go:173-197, streaming8.go:318-340)
             for j, w in enumerate(outputs):
                 if w is not None:
                     _write(w, rows[self.k + j][:al], self.k + j)
@@ -222,11 +230,11 @@ class StreamEncoder16:
 
     # ------------------------------------------------------------------ verify
     def verify(self, shards: Sequence) -> bool:
-        """rsStream16.verify (streaming16.go:200-317)."""
+        """rsStream16.verify (streaming16.go:200-317) / rsStreamFF8.verify
+        (streaming8.go:343-444)."""
         if len(shards) != self.total:
             raise ErrTooFewShards("too few shards given")
         bufs = self._buffers()
-        hist = _GoBufferHistory(self.total)
         pending = deque()
         verdict = [True]
 
@@ -234,6 +242,12 @@ class StreamEncoder16:
             t = pending.popleft()
             if not t.result():
                 verdict[0] = False
+
+        def settle() -> bool:
+            # the reference returns an earlier block's mismatch before anything later
+            while pending and verdict[0]:
+                drain_one()
+            return verdict[0]
 
         blk, read = 0, 0
         try:
@@ -243,74 +257,59 @@ class StreamEncoder16:
                     if not verdict[0]:
                         break
                 rows = bufs[blk % self.depth]
-                size, lens = -1, []
-                for i, rd in enumerate(shards):
-                    if rd is None:
-                        lens.append(0)
-                        continue
-                    try:
-                        n = _read_full(rd, rows[i][:self.block_size])
-                    except Exception as e:
-                        while pending and verdict[0]:  # the reference returns an earlier mismatch first
-                            drain_one()
-                        if not verdict[0]:
-                            return False
-                        raise StreamReadError(e, i) from e
-                    if size == -1 and n > 0:
-                        size = n
-                    lens.append(n)
+                lens = []
+                try:
+                    size = self._read_rows(shards, rows, lens)
+                except StreamReadError:
+                    if not settle():
+                        return False
+                    raise
                 if size <= 0:
-                    while pending and verdict[0]:
-                        drain_one()
-                    if not verdict[0]:
+                    if not settle():
                         return False
                     if read == 0:
                         raise ErrShardNoData("no shard data")
                     return True
-                for i, n in enumerate(lens):  # zero-extend short rows (:245-270)
+                for i, n in enumerate(lens):  # zero-extend short rows, truncate long ones
                     if n < size:
                         rows[i][n:size] = 0
-                if size % 2:  # pad to even with a zero (:274-287)
-                    rows_pad = size + 1
+                if self.EVEN and size % 2:  # pad to even with a zero (streaming16.go:274-287)
                     for r in rows:
                         r[size] = 0
-                    size = rows_pad
-                hist.record([max(n, size) for n in lens])
+                    size += 1
                 al = _ceil64(size)
-                if al > size:  # the 64-byte pad keeps the buffer's old bytes (:290-309)
-                    hist.fill(blk, bufs, size, al)
+                for r in rows:  # zero pad to 64 (streaming16.go:297-305, streaming8.go:420-434)
+                    r[size:al] = 0
                 read += size
                 pending.append(self.rs.verify_async([r[:al] for r in rows]))
                 blk += 1
+                if self.EVEN and size < al < self.block_size:
+                    # every row is now a zeroed buffer of capacity alignedSize
+                    # (streaming16.go:297): a True verdict sends the reference
+                    # into all[i][:r.blockSize] (:218), which panics
+                    if not settle():
+                        return False
+                    raise ErrPanic("streaming16.go:218: slice bounds out of range [:%d] with capacity %d "
+                                   "(the verify loop continues past a block of %d bytes)"
+                                   % (self.block_size, al, size))
             return False
         finally:
             while pending:
                 pending.popleft().wait()
 
     # ------------------------------------------------------------------ reconstruct
-    def reconstruct(self, inputs: Sequence, outputs: Sequence) -> None:
-        """rsStream16.reconstruct (streaming16.go:320-468)."""
+    def _check_io(self, inputs, outputs) -> None:
         if len(inputs) != self.total or len(outputs) != self.total:
             raise ErrTooFewShards("too few shards given")
-        data_only = True
         for i in range(self.total):
             if inputs[i] is not None and outputs[i] is not None:
                 raise ErrReconstructMismatch("a shard cannot be both an input and an output")
-            if i >= self.k and outputs[i] is not None:
-                data_only = False
-        missing = [inputs[i] is None and outputs[i] is not None for i in range(self.total)]
-        if not any(missing):
-            return
-        self._reconstruct_loop(inputs, outputs, missing, recover_all=not data_only, data_loop=False)
 
     def reconstruct_data(self, inputs: Sequence, outputs: Sequence) -> None:
-        """rsStream16.reconstructData (streaming16.go:471-632): rebuilds only
+        """rsStream16.reconstructData (streaming16.go:471-632) /
+        rsStreamFF8.reconstructData (streaming8.go:609-766): rebuilds only
         missing data shards; a nil parity input is fed as a zero shard."""
-        if len(inputs) != self.total or len(outputs) != self.total:
-            raise ErrTooFewShards("too few shards given")
-        for i in range(self.total):
-            if inputs[i] is not None and outputs[i] is not None:
-                raise ErrReconstructMismatch("a shard cannot be both an input and an output")
+        self._check_io(inputs, outputs)
         missing = [i < self.k and inputs[i] is None and outputs[i] is not None for i in range(self.total)]
         self._reconstruct_loop(inputs, outputs, missing, recover_all=False, data_loop=True)
 
@@ -327,7 +326,7 @@ class StreamEncoder16:
                 if data_loop:
                     if i >= self.k:
                         continue
-                    ws = size  # streaming16.go:618-630
+                    ws = size  # streaming16.go:618-630, streaming8.go:752-764
                 else:
                     ws = size if i < self.k else al  # streaming16.go:445-464
                 _write(w, np.asarray(blk_shards[i])[:ws], i)
@@ -338,18 +337,8 @@ class StreamEncoder16:
                 if len(pending) == self.depth:
                     drain_one()
                 rows = bufs[blk % self.depth]
-                size, lens = (-1 if data_loop else 0), []
-                for i, rd in enumerate(inputs):
-                    if rd is None:
-                        lens.append(0)
-                        continue
-                    try:
-                        n = _read_full(rd, rows[i][:self.block_size])
-                    except Exception as e:
-                        raise StreamReadError(e, i) from e
-                    if n > 0 and size <= 0:
-                        size = n
-                    lens.append(n)
+                lens = []
+                size = self._read_rows(inputs, rows, lens)
                 if size <= 0:
                     if read == 0:
                         raise ErrShardNoData("no shard data")
@@ -378,3 +367,68 @@ class StreamEncoder16:
         finally:
             while pending:
                 drain_one()
+
+
+class StreamEncoder16(_StreamCodec):
+    """rsStream16 (streaming16.go:16-71) over the MI355X engine.
+
+    ``encode(inputs, outputs)``, ``verify(shards)``, ``reconstruct(inputs,
+    outputs)`` and ``reconstruct_data(inputs, outputs)`` take file-like readers
+    (``readinto`` or ``read``; None = a nil reader) and writers (``write``;
+    None = nil), like the Go io.Reader / io.Writer slices."""
+
+    FIELD = 16
+    EVEN = True
+
+    def reconstruct(self, inputs: Sequence, outputs: Sequence) -> None:
+        """rsStream16.reconstruct (streaming16.go:320-468)."""
+        if len(inputs) != self.total or len(outputs) != self.total:
+            raise ErrTooFewShards("too few shards given")
+        data_only = True
+        for i in range(self.total):
+            if inputs[i] is not None and outputs[i] is not None:
+                raise ErrReconstructMismatch("a shard cannot be both an input and an output")
+            if i >= self.k and outputs[i] is not None:
+                data_only = False
+        missing = [inputs[i] is None and outputs[i] is not None for i in range(self.total)]
+        if not any(missing):
+            return
+        self._reconstruct_loop(inputs, outputs, missing, recover_all=not data_only, data_loop=False)
+
+
+class StreamEncoder8(_StreamCodec):
+    """rsStreamFF8 (streaming8.go:50-101) over the MI355X engine: the stream
+    codec ``New`` selects for k + p <= 256.  Same methods as StreamEncoder16."""
+
+    FIELD = 8
+    EVEN = False
+
+    def reconstruct(self, inputs: Sequence, outputs: Sequence) -> None:
+        """rsStreamFF8.reconstruct (streaming8.go:447-606).  Every nil input,
+        the requested outputs included, becomes a zero row of the block size
+        (:389-393, :507-532), so ``r.rs.Reconstruct`` finds every shard
+        present and returns at once (leopard8.go:459-462): each requested
+        output receives zeros, ``size`` bytes per data shard and
+        ``ceil64(size)`` per parity shard (:586-604)."""
+        self._check_io(inputs, outputs)
+        recover_all = any(outputs[i] is not None for i in range(self.k, self.total))  # :459-467
+        bufs = self._buffers()
+        blk, read = 0, 0
+        while True:
+            rows = bufs[blk % self.depth]
+            lens = []
+            size = self._read_rows(inputs, rows, lens)
+            if size <= 0:
+                if read == 0:
+                    raise ErrShardNoData("no shard data")
+                return
+            al = _ceil64(size)
+            for i, n in enumerate(lens):
+                rows[i][min(n, size):al] = 0
+            t = self.rs.reconstruct_async([r[:al] for r in rows], recover_all)  # all present: a no-op
+            t.wait()
+            read += size
+            for i, w in enumerate(outputs):
+                if w is not None:
+                    _write(w, rows[i][:size if i < self.k else al], i)
+            blk += 1

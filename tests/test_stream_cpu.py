@@ -1,17 +1,19 @@
-"""The pipelined stream mirror (reedsolomon16_amd/stream.py) against the
-single-buffer restatement of rsStream16 (tests/go_stream.py), on the CPU: the
-codec behind the mirror is an oracle-backed stand-in with the engine's ticket
-API, so these tests check the block logic (sizes, padding, truncation, the
-verify loop's stale 64-byte pad, output sizes, block order, depth rotation).
-The same comparisons run through the HIP engine in test_gpu_stream.py."""
+"""The pipelined stream mirrors (reedsolomon16_amd/stream.py) against the
+single-buffer restatements of rsStream16 and rsStreamFF8 (tests/go_stream.py),
+on the CPU: the codec behind the mirror is an oracle-backed stand-in with the
+engine's ticket API, so these tests check the block logic (sizes, padding,
+truncation, the verify loop's zeroed 64-byte pad and the panic after it,
+output sizes, block order, depth rotation).  The same comparisons run through
+the HIP engine in test_gpu_stream.py."""
 import io
 
 import numpy as np
 import pytest
 
 from oracle.orc import Oracle
-from reedsolomon16_amd.stream import StreamEncoder16
-from tests.go_stream import GoStream16
+from reedsolomon16_amd.codec import ErrPanic
+from reedsolomon16_amd.stream import StreamEncoder8, StreamEncoder16
+from tests.go_stream import GoPanic, GoStream8, GoStream16
 
 
 class _Ticket:
@@ -34,9 +36,9 @@ class OracleTicketCodec:
     """Oracle stand-in for reedsolomon16_amd.codec.ReedSolomon's ticket API
     (test infrastructure: records what the stream hands the codec)."""
 
-    def __init__(self, k, p):
+    def __init__(self, k, p, bits=16):
         self.k, self.p, self.total = k, p, k + p
-        self.orc = Oracle(16, k, p)
+        self.orc = Oracle(bits, k, p)
         self.calls = []
 
     def alloc_aligned(self, each, shards=None, pinned=False):
@@ -81,9 +83,10 @@ def _streams(datas):
     return [None if d is None else io.BytesIO(d) for d in datas]
 
 
-def _mirror(k, p, depth=2):
-    fake = OracleTicketCodec(k, p)
-    return StreamEncoder16(k, p, block_size=BLOCK, depth=depth, codec=fake), fake
+def _mirror(k, p, depth=2, bits=16):
+    fake = OracleTicketCodec(k, p, bits)
+    cls = StreamEncoder16 if bits == 16 else StreamEncoder8
+    return cls(k, p, block_size=BLOCK, depth=depth, codec=fake), fake
 
 
 def _data(rng, lens):
@@ -126,7 +129,16 @@ def _encoded_stream(k, p, n, seed):
     return datas, [o.getvalue() for o in outs]
 
 
-@pytest.mark.parametrize("n", [768, 999, 700, 62])
+def _outcome(fn, *args):
+    """A verify verdict, or "panic" for the reference's Go panic / the
+    mirror's ErrPanic."""
+    try:
+        return fn(*args)
+    except (GoPanic, ErrPanic):
+        return "panic"
+
+
+@pytest.mark.parametrize("n", [768, 999, 700, 62, 20, 130])
 @pytest.mark.parametrize("tamper", [None, 0, 7])
 def test_stream_verify_matches_go_loop(n, tamper):
     k, p = 5, 3
@@ -137,30 +149,113 @@ def test_stream_verify_matches_go_loop(n, tamper):
         b[min(300, len(b) - 1)] ^= 1
         shards[tamper] = bytes(b)
     go = GoStream16(k, p, BLOCK)
-    gv = go.verify(_streams(shards))
+    gv = _outcome(go.verify, _streams(shards))
     st, fake = _mirror(k, p)
-    mv = st.verify(_streams(shards))
-    assert mv == gv
+    assert _outcome(st.verify, _streams(shards)) == gv
     # every block the reference verified was verified with the same bytes
     # (the mirror may have queued one more block after a mismatch)
     assert fake.calls[:len(go.calls)] == go.calls
 
 
-def test_stream_verify_stale_pad_is_reference_behaviour():
-    """A multi-block stream whose last block is not 64-aligned: the reference's
-    verify pads it with the previous block's bytes (streaming16.go:290-309),
-    so it reports a mismatch for a stream its own encode produced."""
-    k, p = 4, 2
-    datas, par = _encoded_stream(k, p, BLOCK + 100, 3)
+@pytest.mark.parametrize("k,p,n,want", [
+    # 4 + 2 has only GF(2^8) twiddles: a parity symbol's high byte depends on
+    # the data's high bytes alone, the zero pad (which covers every high byte
+    # the data lacks) drops zero parity, the block verifies, and the next
+    # all[i][:r.blockSize] (:218) panics -- a single block as the tail of a
+    # multi-block stream, whichever half the pad starts in
+    (4, 2, BLOCK + 20, "panic"), (4, 2, 20, "panic"), (4, 2, 130, "panic"),
+    (4, 2, BLOCK + 100, "panic"), (4, 2, 100, "panic"), (4, 2, 62, "panic"),
+    # padded up to exactly blockSize: the capacity stays blockSize, no panic
+    (4, 2, 2 * BLOCK - 10, True),
+    # 300 + 4: chunk twiddles from fftSkew[255] on are full-field, so the pad
+    # drops nonzero parity bytes and the block verifies False
+    (300, 4, BLOCK + 20, False), (300, 4, 100, False), (300, 4, 62, False),
+])
+def test_stream_verify_unaligned_last_block_is_zero_padded(k, p, n, want):
+    """streaming16.go:290-309: every row reaching :295 is `size` bytes long, so
+    each becomes a fresh zeroed buffer of alignedSize; the parity rows' real
+    bytes past `size` are replaced by zeros."""
+    datas, par = _encoded_stream(k, p, n, n + k)
     go = GoStream16(k, p, BLOCK)
-    assert go.verify(_streams(list(datas) + par)) is False
+    assert _outcome(go.verify, _streams(list(datas) + par)) == want
     st, fake = _mirror(k, p)
-    assert st.verify(_streams(list(datas) + par)) is False
+    assert _outcome(st.verify, _streams(list(datas) + par)) == want
     assert fake.calls == go.calls
-    # a single-block stream (fresh, zeroed buffer) verifies
-    datas, par = _encoded_stream(k, p, 100, 4)
-    assert GoStream16(k, p, BLOCK).verify(_streams(list(datas) + par)) is True
-    assert _mirror(k, p)[0].verify(_streams(list(datas) + par)) is True
+    # the codec saw zeros past `size` in every row, parity included
+    size = (n - 1) % BLOCK + 1
+    size += size % 2
+    assert all(set(r[size:]) <= {0} for r in go.calls[-1][1])
+    if want is not True:
+        assert any(set(r[size:]) != {0} for r in par_blocks(par, len(go.calls) - 1)) == (want is False)
+
+
+def par_blocks(par, blk):
+    return [np.frombuffer(x, np.uint8)[blk * BLOCK:(blk + 1) * BLOCK] for x in par]
+
+
+def test_stream_verify_true_on_unaligned_block_panics():
+    """If the zero-padded block verifies (here: all-zero shards), the reference
+    loops back to all[i][:r.blockSize] (streaming16.go:218) on a row whose
+    capacity is now alignedSize, and panics; the mirror raises ErrPanic there.
+    A tail whose alignedSize equals blockSize keeps the capacity and ends
+    normally."""
+    k, p = 4, 2
+    shards = [bytes(100)] * k + [bytes(128)] * p
+    with pytest.raises(GoPanic):
+        GoStream16(k, p, BLOCK).verify(_streams(shards))
+    st, fake = _mirror(k, p)
+    with pytest.raises(ErrPanic):
+        st.verify(_streams(shards))
+    assert len(fake.calls) == 1
+    # an aligned all-zero stream verifies and ends normally
+    shards = [bytes(2 * BLOCK)] * k + [bytes(2 * BLOCK)] * p
+    assert GoStream16(k, p, BLOCK).verify(_streams(shards)) is True
+    assert _mirror(k, p)[0].verify(_streams(shards)) is True
+    # a tail padded up to exactly blockSize
+    shards = [bytes(2 * BLOCK - 10)] * k + [bytes(2 * BLOCK)] * p
+    assert GoStream16(k, p, BLOCK).verify(_streams(shards)) is True
+    assert _mirror(k, p)[0].verify(_streams(shards)) is True
+    # a multi-block zero stream with an unaligned tail: full blocks verify,
+    # the tail verifies, then the reference panics
+    shards = [bytes(BLOCK + 70)] * k + [bytes(BLOCK + 128)] * p
+    with pytest.raises(GoPanic):
+        GoStream16(k, p, BLOCK).verify(_streams(shards))
+    with pytest.raises(ErrPanic):
+        _mirror(k, p, depth=3)[0].verify(_streams(shards))
+
+
+# row-length classes at streaming16.go:295-302: the block size (aligned, odd,
+# even and unaligned in the low / high half of a 64-byte block) and each
+# row's own length (exact, short -> zero-extended, long -> truncated, nil)
+VERIFY_ROW_CLASSES = {
+    "aligned": (128, [128, 128, 128, 128, 128, 128]),
+    "odd": (99, [99, 99, 50, 99, 99, 99]),
+    "odd_to_64": (63, [63, 63, 63, 63, 63, 64]),
+    "even_low_half": (20, [20, 7, 20, None, 20, 64]),
+    "even_high_half": (52, [52, 52, 80, 52, 64, 64]),
+    "two_blocks_tail_low": (BLOCK + 2, [BLOCK + 2] * 4 + [BLOCK + 64] * 2),
+    "two_blocks_tail_high": (BLOCK + 90, [BLOCK + 90, BLOCK + 91, BLOCK + 1, BLOCK + 90, BLOCK + 128, BLOCK + 128]),
+}
+
+
+@pytest.mark.parametrize("case", sorted(VERIFY_ROW_CLASSES))
+@pytest.mark.parametrize("zero", [False, True])
+def test_stream_verify_row_length_classes(case, zero):
+    k, p = 4, 2
+    n, lens = VERIFY_ROW_CLASSES[case]
+    rng = np.random.default_rng(len(case))
+    if zero:
+        shards = [None if m is None else bytes(m) for m in lens]
+    else:
+        datas, par = _encoded_stream(k, p, n, len(case))
+        shards = [None if m is None else (d * 2)[:m] for d, m in zip(list(datas) + par, lens)]
+    go = GoStream16(k, p, BLOCK)
+    want = _outcome(go.verify, _streams(shards))
+    st, fake = _mirror(k, p)
+    assert _outcome(st.verify, _streams(shards)) == want
+    assert fake.calls[:len(go.calls)] == go.calls
+    if zero:
+        assert want == ("panic" if (n + n % 2) % 64 else True)
 
 
 @pytest.mark.parametrize("n", [768, 999, 130])
@@ -265,3 +360,100 @@ def test_stream_write_order_and_read_error_after_blocks():
     with pytest.raises(StreamReadError):
         st.encode([io.BytesIO(datas[0])] + [FailThird(d) for d in datas[1:]], out)
     assert [o.getvalue() for o in out] == [o.getvalue() for o in ref]
+
+
+# --------------------------------------------------------------------------- rsStreamFF8
+def _encoded_stream8(k, p, n, seed):
+    rng = np.random.default_rng(seed)
+    datas = _data(rng, [n] * k)
+    go = GoStream8(k, p, BLOCK)
+    outs = [io.BytesIO() for _ in range(p)]
+    go.encode(_streams(datas), outs)
+    return datas, [o.getvalue() for o in outs]
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3])
+@pytest.mark.parametrize("case", sorted(ENC_CASES))
+def test_stream8_encode_matches_go_loop(case, depth):
+    """streaming8.go:109-181: no even step, zero pad to 64, ceil64(size) parity bytes."""
+    k, p = 6, 3
+    rng = np.random.default_rng(len(case) * 11 + depth)
+    datas = _data(rng, ENC_CASES[case])
+    go = GoStream8(k, p, BLOCK)
+    gout = [io.BytesIO() for _ in range(p)]
+    go.encode(_streams(datas), gout)
+    st, fake = _mirror(k, p, depth, bits=8)
+    mout = [io.BytesIO() for _ in range(p)]
+    st.encode(_streams(datas), mout)
+    assert fake.calls == go.calls
+    assert [o.getvalue() for o in mout] == [o.getvalue() for o in gout]
+
+
+@pytest.mark.parametrize("n", [768, 999, 700, 62, 33])
+@pytest.mark.parametrize("tamper", [None, 0, 7])
+def test_stream8_verify_matches_go_loop(n, tamper):
+    """streaming8.go:343-444: the block buffer keeps its capacity and the pad
+    is zeroed, so an unaligned tail verifies (byte columns are independent)."""
+    k, p = 5, 3
+    datas, par = _encoded_stream8(k, p, n, n)
+    shards = list(datas) + list(par)
+    if tamper is not None:
+        b = bytearray(shards[tamper])
+        b[min(300, len(b) - 1)] ^= 1
+        shards[tamper] = bytes(b)
+    go = GoStream8(k, p, BLOCK)
+    gv = go.verify(_streams(shards))
+    st, fake = _mirror(k, p, bits=8)
+    assert st.verify(_streams(shards)) == gv
+    assert fake.calls[:len(go.calls)] == go.calls
+    if tamper is None:
+        assert gv is True
+
+
+@pytest.mark.parametrize("n", [768, 999, 130])
+@pytest.mark.parametrize("erase", [(0,), (1, 6), (0, 2, 5)])
+def test_stream8_reconstruct_data_matches_go_loop(n, erase):
+    """streaming8.go:609-766 (what StreamReconstruct runs when only data
+    outputs are requested, reedsolomon.go:174-185): rebuilds the data shards."""
+    k, p = 5, 3
+    datas, par = _encoded_stream8(k, p, n, n + 3)
+    shards = list(datas) + list(par)
+    mk_in = lambda: [None if i in erase else io.BytesIO(shards[i]) for i in range(k + p)]
+    go_out = [io.BytesIO() if i in erase and i < k else None for i in range(k + p)]
+    go = GoStream8(k, p, BLOCK)
+    go.reconstruct_data(mk_in(), go_out)
+    m_out = [io.BytesIO() if i in erase and i < k else None for i in range(k + p)]
+    st, fake = _mirror(k, p, bits=8)
+    st.reconstruct_data(mk_in(), m_out)
+    assert fake.calls == go.calls
+    for i in erase:
+        if i < k:
+            assert m_out[i].getvalue() == go_out[i].getvalue()
+            # a nil parity input is fed as a zero shard (:680-685), so the
+            # rebuilt data is right only when every parity shard is read
+            assert (go_out[i].getvalue() == shards[i]) == all(j < k for j in erase)
+
+
+@pytest.mark.parametrize("n", [768, 130])
+def test_stream8_reconstruct_writes_zeros_like_the_reference(n):
+    """streaming8.go:447-606 zero-extends every nil input (:389-393), so the
+    codec sees all shards present and returns at once (leopard8.go:459-462),
+    and every requested output receives zeros: `size` bytes per data shard,
+    ceil64(size) per parity shard."""
+    k, p = 5, 3
+    datas, par = _encoded_stream8(k, p, n, 21)
+    shards = list(datas) + list(par)
+    erase = (1, 6)
+    mk_in = lambda: [None if i in erase else io.BytesIO(shards[i]) for i in range(k + p)]
+    go_out = [io.BytesIO() if i in erase else None for i in range(k + p)]
+    go = GoStream8(k, p, BLOCK)
+    go.reconstruct(mk_in(), go_out)
+    m_out = [io.BytesIO() if i in erase else None for i in range(k + p)]
+    st, fake = _mirror(k, p, bits=8)
+    st.reconstruct(mk_in(), m_out)
+    assert [c[0] for c in fake.calls] == [c[0] for c in go.calls]
+    assert all(None not in c[1] for c in go.calls)  # nothing missing in any call
+    for i in erase:
+        assert m_out[i].getvalue() == go_out[i].getvalue()
+    assert go_out[1].getvalue() == bytes(n)
+    assert go_out[6].getvalue() == bytes((n + 63) // 64 * 64)
