@@ -33,8 +33,10 @@ the kernel timing with one stripe per launch (the reference's Encode
 granularity).  Resident rows sit at a stride of row bytes + --row-pad (3.5 KiB
 by default); `unpadded_rows` times the same launch on rows
 packed exactly one row length apart.  `other_workloads` (one GPU) reports the
-kernel time and roofline fraction of the C4 reconstruct and the C5 encode
-beside the headline.  `cpu_baseline` times the reference-equivalent AVX2 and AVX-512 ports of the
+kernel time and roofline fraction of the C2 encode, the C4 reconstruct and
+the C5 encode and repair beside the headline; `host_resident` the
+PCIe-inclusive rates with the shards in host memory (the engine's tickets and
+the rsStream16 mirror at 4 MiB blocks).  `cpu_baseline` times the reference-equivalent AVX2 and AVX-512 ports of the
 encode (oracle/leopard_ref.c, test/bench infrastructure) on a bounded sample:
 1 thread (the reference is single-threaded per call) and N threads over byte
 ranges.
@@ -195,6 +197,165 @@ def other_workloads(torch, rs, dev, stream) -> dict:
     return out
 
 
+def c2_encode(torch, rs, dev, stream) -> dict:
+    """C2 (BASELINE configs[1]): GF(2^8) encode of 10 + 4 x 1 MiB
+    (leopard8.go:153-277), one stripe per launch and 16 stripes per launch
+    (rs_encode_dev_batch), HIP-event kernel time on the launch stream.
+    Algorithmic bytes (k + p) * S per stripe."""
+    k, p, S = 10, 4, 1 << 20
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xC2)
+    c2 = rs.New8(k, p, device=dev.index)
+    slab = torch.randint(0, 256, (16, k + p, S), dtype=torch.uint8, device=dev, generator=g)
+    out = {"config": "10+4 x 1024 KiB, GF(2^8)", "kernel_path": c2.encode_path}
+    for ns, reps in ((1, 400), (16, 100)):
+        view = slab[:ns]
+        for _ in range(10):
+            c2.encode_dev_batch(view, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(reps):
+            c2.encode_dev_batch(view, stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        alg = ns * (k + p) * S
+        out[f"stripes_{ns}"] = {"kernel_ms": round(ms, 5), "us_per_stripe": round(ms * 1e3 / ns, 3),
+                                "alg_bytes_per_launch": alg,
+                                "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    del slab
+    return out
+
+
+class _ArrayReader:
+    """io.Reader over a numpy byte array (readinto copies, as io.ReadFull does)."""
+
+    def __init__(self, a):
+        self.a, self.off = a, 0
+
+    def readinto(self, b):
+        n = min(len(b), len(self.a) - self.off)
+        if n <= 0:
+            return 0
+        b[:n] = memoryview(self.a)[self.off:self.off + n]
+        self.off += n
+        return n
+
+
+class _ArrayWriter:
+    """io.Writer into a preallocated numpy byte array."""
+
+    def __init__(self, a):
+        self.a, self.off = a, 0
+
+    def write(self, b):
+        n = len(b)
+        self.a[self.off:self.off + n] = b
+        self.off += n
+        return n
+
+
+def host_resident(rs, blocks: int = 2, block: int = 4 << 20) -> dict:
+    """The north star's host-resident rate (PCIe-inclusive; never `value`):
+    128 + 32 shards in host memory, rsStream16's 4 MiB blocks.
+      tickets: the engine's async host entry points on pinned blocks
+               (rs_encode_async / rs_verify_async / rs_reconstruct_async,
+               32 erasures into pinned EmptyShard rows), `blocks` stripes
+               queued back to back -- the codec side of the stream loop;
+      stream:  the rsStream16 mirror (reedsolomon16_amd/stream.py
+               StreamEncoder16, streaming16.go:200-468,1229-1318) over
+               in-memory readers and writers, so io.ReadFull's copy into the
+               block buffer and the output writes are inside the time.
+    data GiB/s = k * bytes per shard / time; PCIe GB/s = bytes crossing the
+    link / time (encode: k in + p out, verify: k + p in, reconstruct:
+    present in + rebuilt out)."""
+    import numpy as np
+
+    from reedsolomon16_amd.stream import StreamEncoder16
+
+    K, P = 128, 32
+    L = blocks * block
+    codec = rs.New16(K, P)
+    rng = np.random.default_rng(0x5EED)
+    data = rs.alloc_pinned(K * L).reshape(K, L)
+    data[:] = rng.integers(0, 256, data.shape, dtype=np.uint8)
+    par = rs.alloc_pinned(P * L).reshape(P, L)
+    erased = sorted(np.random.default_rng(0xC4).choice(K + P, P, replace=False).tolist())
+    out = {"config": f"{K}+{P} shards, {blocks} blocks of {block >> 20} MiB per shard, {len(erased)} erasures"}
+
+    def rate(op, t, read_rows, write_rows):
+        return {"ms": round(t * 1e3, 3), "data_gib_s": round(K * L / t / 2**30, 3),
+                "pcie_gb_s": round((read_rows + write_rows) * L / t / 1e9, 3)}
+
+    # ---- tickets on pinned blocks
+    rows = [[data[i, b * block:(b + 1) * block] for i in range(K)] +
+            [par[j, b * block:(b + 1) * block] for j in range(P)] for b in range(blocks)]
+
+    def enc():
+        ts = [codec.encode_async(r) for r in rows]
+        for t in ts:
+            t.wait()
+
+    def ver():
+        ts = [codec.verify_async(r) for r in rows]
+        assert all(t.result() for t in ts)
+
+    rebuilt = rs.alloc_pinned(len(erased) * block * blocks).reshape(blocks, len(erased), block)
+
+    def rec():
+        ts = []
+        for b, r in enumerate(rows):
+            sh = list(r)
+            for j, i in enumerate(erased):
+                sh[i] = rs.EmptyShard(rebuilt[b, j])
+            ts.append(codec.reconstruct_async(sh, True))
+        for t in ts:
+            t.wait()
+
+    tick = {}
+    for name, fn, rd, wr in (("encode", enc, K, P), ("verify", ver, K + P, 0),
+                             ("reconstruct", rec, K + P - len(erased), len(erased))):
+        fn()  # warm: plans, staging buffers
+        t0 = time.perf_counter()
+        fn()
+        tick[name] = rate(name, time.perf_counter() - t0, rd, wr)
+    for j, i in enumerate(erased):
+        src = data[i] if i < K else par[i - K]
+        assert all(np.array_equal(rebuilt[b, j], src[b * block:(b + 1) * block]) for b in range(blocks))
+    out["tickets"] = tick
+
+    # ---- the rsStream16 mirror over readers / writers
+    st = StreamEncoder16(K, P, block_size=block)
+    sink = np.empty((P, L), np.uint8)
+    stream_rates = {}
+
+    def s_enc():
+        st.encode([_ArrayReader(data[i]) for i in range(K)], [_ArrayWriter(sink[j]) for j in range(P)])
+
+    def s_ver():
+        assert st.verify([_ArrayReader(data[i]) for i in range(K)] + [_ArrayReader(par[j]) for j in range(P)])
+
+    rsink = np.empty((len(erased), L), np.uint8)
+
+    def s_rec():
+        ins = [None if i in erased else _ArrayReader(data[i] if i < K else par[i - K]) for i in range(K + P)]
+        outs = [None] * (K + P)
+        for j, i in enumerate(erased):
+            outs[i] = _ArrayWriter(rsink[j])
+        st.reconstruct(ins, outs)
+
+    for name, fn, rd, wr in (("encode", s_enc, K, P), ("verify", s_ver, K + P, 0),
+                             ("reconstruct", s_rec, K + P - len(erased), len(erased))):
+        fn()
+        t0 = time.perf_counter()
+        fn()
+        stream_rates[name] = rate(name, time.perf_counter() - t0, rd, wr)
+    assert np.array_equal(sink, par)
+    out["stream"] = stream_rates
+    return out
+
+
 def free_port() -> int:
     import socket
 
@@ -266,6 +427,7 @@ def main():
     ap.add_argument("--no-unpadded", action="store_true", help="skip timing the unpadded layout")
     ap.add_argument("--dry-run", action="store_true", help="rank layout only: gloo on the CPU, no GPU")
     ap.add_argument("--no-other", action="store_true", help="skip the C4 / C5 kernel figures (one GPU only)")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-resident (PCIe-inclusive) figures")
     ap.add_argument("--slice-of", type=int, default=0,
                     help="one GPU: encode rank 0's byte range of an N-rank split (the launch shape each rank of an "
                          "N-GPU run has, for its rocprofv3 PMC passes); not a job-throughput figure")
@@ -369,11 +531,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el, kern_ms, one_ms, flat_ms = float(t[0]), float(t[1]), float(t[2]) or None, float(t[3]) or None
 
-    other = None
+    other = host = None
     if world == 1 and not args.no_other:
         del buf, slab, flat
         torch.cuda.empty_cache()
         other = other_workloads(torch, rs, dev, stream)
+        other["C2_encode"] = c2_encode(torch, rs, dev, stream)
+        torch.cuda.empty_cache()
+    if world == 1 and not args.no_host:
+        host = host_resident(rs)
 
     ms_per_step = el / args.steps * 1e3
     job_stripes = B if args.split == "bytes" else world * B
@@ -445,6 +611,7 @@ def main():
             # rank 0 only, after the timed region (the other ranks wait at the barrier below)
             "cpu_baseline": None if args.no_cpu else cpu_baseline(K, P, S, args.cpu_seconds, threads),
             "other_workloads": other,
+            "host_resident": host,
         }
         print(json.dumps(res), flush=True)
     if world > 1:

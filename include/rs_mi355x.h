@@ -249,6 +249,15 @@ int rs_debug_split_emulate(rs_codec *codec, const uint8_t *data, uint8_t *parity
  * Returns 0, or -1 when the kernel does not serve mtrunc.  Host only. */
 int rs_debug_dec_plan(int mtrunc, const uint32_t *need, uint64_t *code);
 
+/* Test-only kernel-path overrides (process-wide), so the parity tests can run
+ * the variants other geometries select on the same small inputs:
+ *   "bs" 0/1          bit-sliced GF(2^16) encode off / on (default 1; read by rs_new),
+ *   "sub" 0/1         subfield-coordinate transforms off / on (default 1),
+ *   "prune" 0/1       errorBitfield pruning of the reconstruct FFT off / on (default 1),
+ *   "unit_width" -1/0/1  LDS and GF(2^8) register units automatic / wide / narrow (default -1).
+ * Returns RS_ERR_INVALID_ARG for an unknown knob or value.  Host only. */
+int rs_debug_set_path(const char *knob, int value);
+
 /* Human-readable message for an error code. */
 const char *rs_strerror(int code);
 

@@ -73,8 +73,23 @@ def lib() -> C.CDLL:
     L.rs_debug_sub_swap.argtypes = [C.c_uint32]
     L.rs_debug_sub_swap.restype = C.c_uint32
     L.rs_debug_dec_plan.argtypes = [i32, vp, vp]
+    L.rs_debug_set_path.argtypes = [C.c_char_p, i32]
     _lib = L
     return L
+
+
+_PATH_DEFAULTS = {"bs": 1, "sub": 1, "prune": 1, "unit_width": -1}
+
+
+def set_path(knob: str, value: int) -> None:
+    """rs_debug_set_path: a test-only kernel-path override (include/rs_mi355x.h)."""
+    if lib().rs_debug_set_path(knob.encode(), int(value)) != 0:
+        raise ValueError("unknown path knob %r = %r" % (knob, value))
+
+
+def reset_paths() -> None:
+    for k, v in _PATH_DEFAULTS.items():
+        set_path(k, v)
 
 
 def header_functions() -> list[str]:

@@ -99,6 +99,27 @@ def alloc_pinned(nbytes: int) -> np.ndarray:
     return a
 
 
+class _PinnedArena:
+    """Sub-allocates pinned rows from 64 MiB rs_host_alloc blocks, so a
+    reconstruct ticket's fresh output rows do not each pay for a page-locking
+    allocation.  A block is freed when the last row cut from it is gone."""
+
+    BLOCK = 64 << 20
+
+    def __init__(self):
+        self._cur, self._off = None, 0
+
+    def take(self, nbytes: int) -> np.ndarray:
+        need = (nbytes + 63) // 64 * 64
+        if nbytes > self.BLOCK // 4:
+            return alloc_pinned(nbytes)
+        if self._cur is None or self._off + need > len(self._cur):
+            self._cur, self._off = alloc_pinned(self.BLOCK), 0
+        row = self._cur[self._off:self._off + nbytes]
+        self._off += need
+        return row
+
+
 class EmptyShard:
     """A missing shard that keeps its memory, like Go's ``shards[i][:0]``:
     length 0 (so Reconstruct treats it as missing) and capacity ``len(buf)``.
@@ -207,6 +228,7 @@ class ReedSolomon:
         self._h = h
         self._L = L
         self.device = device
+        self._arena = _PinnedArena()
 
     def close(self):
         if getattr(self, "_h", None):
@@ -319,8 +341,11 @@ class ReedSolomon:
                 bufs[i] = _capacity_view(bufs[i], S)
                 if bufs[i] is None:
                     # a ticket's rebuilt rows go into pinned memory: pageable
-                    # outputs would make the queued call synchronous (bounce slab)
-                    bufs[i] = alloc_pinned(S) if ticket else np.empty(S, dtype=np.uint8)
+                    # outputs would make the queued call synchronous (bounce slab).
+                    # Callers that loop over stripes pass EmptyShard(row) of their
+                    # own pinned rows instead (stream.py does); otherwise the rows
+                    # come from the codec's pinned arena
+                    bufs[i] = self._arena.take(S) if ticket else np.empty(S, dtype=np.uint8)
         ptrs = (C.c_void_p * total)()
         lens = (C.c_size_t * total)()
         for i, s in enumerate(shards):

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <list>
@@ -334,18 +335,18 @@ int upload_split(rs_codec *c) {
     return RS_OK;
 }
 
-// Test-only path overrides.  The parity tests use them to run the kernel
-// variants that other geometries select (the bit-sliced encode off, the
-// transforms in full-field coordinates, the reconstruct FFT unpruned) on the
-// same small inputs; nothing else reads them.  (kernels.hip unit_width_override
-// is the fourth: RS_UNIT_WIDTH.)
-bool env_flag(const char *name, char on) {
-    const char *e = getenv(name);
-    return e && e[0] == on;
-}
-bool bs_enabled() { return !env_flag("RS_BS", '0'); }           // RS_BS=0: no bit-sliced encode
-bool sub_enabled() { return !env_flag("RS_NO_SUB", '1'); }      // RS_NO_SUB=1: full-field coordinates
-bool prune_enabled() { return !env_flag("RS_NO_PRUNE", '1'); }  // RS_NO_PRUNE=1: unpruned reconstruct FFT
+// Test-only path overrides, set through rs_debug_set_path (include/rs_mi355x.h).
+// The parity tests use them to run the kernel variants that other geometries
+// select (the bit-sliced encode off, the transforms in full-field coordinates,
+// the reconstruct FFT unpruned, the narrow / wide LDS units) on the same small
+// inputs.  Process-wide; read when a codec is created (bs) or at each launch.
+std::atomic<int> g_path_bs{1}, g_path_sub{1}, g_path_prune{1}, g_path_unit_width{-1};
+bool bs_enabled() { return g_path_bs.load(std::memory_order_relaxed) != 0; }
+bool sub_enabled() { return g_path_sub.load(std::memory_order_relaxed) != 0; }
+bool prune_enabled() { return g_path_prune.load(std::memory_order_relaxed) != 0; }
+}  // namespace
+int rs::unit_width_override() { return g_path_unit_width.load(std::memory_order_relaxed); }
+namespace {
 
 // Host half of the encode plan (no device calls): twiddle schedule and panic check.
 void plan_encode_host(rs_codec *c) {
@@ -435,7 +436,7 @@ int ensure_device(rs_codec *c) {
 // schedule's own logs: a codec whose slots do not fit stays full-field.
 int upload_big_sub(rs_codec *c, const std::vector<uint32_t> &il, const std::vector<uint32_t> &fl) {
     if (c->bits != 16 || c->logn < 9 || c->logn > kMaxLdsRecLogN16 || !sub_enabled() || !sub_coords().ok) return RS_OK;
-    const int ni = c->logn == 11 ? 2 : 1, fend = 4;
+    const int ni = big_sub_ifft_first(c->logn), fend = big_sub_fft_end(c->logn);
     const auto ip = ifft_passes(c->logn), fp = fft_passes(c->logn);
     auto range = [](const std::vector<PassInfo> &ps, int p, size_t total) {
         return std::make_pair((size_t)ps[p].slot_off, p + 1 < (int)ps.size() ? (size_t)ps[p + 1].slot_off : total);
@@ -755,9 +756,11 @@ std::vector<uint8_t> plan_key(const std::vector<uint8_t> &present, bool recover_
 }
 
 // Plans are cached per (erasure pattern, recover_all): repeated repairs of
-// the same pattern skip the table construction.
-int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, uint64_t S, RecPlan &pl) {
-    const std::vector<uint32_t> *el_ref = ref_inv_errlocs(c, present, recover_all, S);
+// the same pattern skip the table construction.  `el_ref` is the call's one
+// reference-keyed cache answer (ref_inv_errlocs), looked up by the caller
+// exactly once per reconstruct, as leopard8.go:509-554 looks up and stores once.
+int plan_reconstruct_el(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
+                        const std::vector<uint32_t> *el_ref, RecPlan &pl) {
     std::vector<uint8_t> key = plan_key(present, recover_all, el_ref);
     for (auto it = c->plan_cache.begin(); it != c->plan_cache.end(); ++it) {
         if (it->first == key) {
@@ -771,6 +774,9 @@ int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool reco
     c->plan_cache.emplace_front(std::move(key), pl);
     if (c->plan_cache.size() > 16) c->plan_cache.pop_back();
     return RS_OK;
+}
+int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, uint64_t S, RecPlan &pl) {
+    return plan_reconstruct_el(c, present, recover_all, ref_inv_errlocs(c, present, recover_all, S), pl);
 }
 
 int plan_reconstruct_new(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
@@ -901,7 +907,8 @@ void set_big_sub(const rs_codec *c, RecArgs &ra) {
 
 // Device-resident plan for (present, recover_all), built and uploaded on first use.
 int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, uint64_t S, DevPlan **out) {
-    std::vector<uint8_t> key = plan_key(present, recover_all, ref_inv_errlocs(c, present, recover_all, S));
+    const std::vector<uint32_t> *el_ref = ref_inv_errlocs(c, present, recover_all, S);
+    std::vector<uint8_t> key = plan_key(present, recover_all, el_ref);
     for (auto it = c->dplan_cache.begin(); it != c->dplan_cache.end(); ++it) {
         if (it->first == key) {
             c->dplan_cache.splice(c->dplan_cache.begin(), c->dplan_cache, it);
@@ -910,7 +917,7 @@ int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
         }
     }
     auto dp = std::make_unique<DevPlan>();
-    if (int e = plan_reconstruct(c, present, recover_all, S, dp->pl)) return e;
+    if (int e = plan_reconstruct_el(c, present, recover_all, el_ref, dp->pl)) return e;
     const RecPlan &pl = dp->pl;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t s_in = pl.tw_in.size() * 4, s_out = pl.tw_out.size() * 4, s_pos = std::max<size_t>(pl.pos.size(), 1) * 4;
@@ -2125,6 +2132,17 @@ int rs_debug_split_check(int logm, uint32_t seed) {
         case 5: return split_sim<5>(F, seed);
     }
     return -1;
+}
+
+int rs_debug_set_path(const char *knob, int value) {
+    if (!knob) return RS_ERR_INVALID_ARG;
+    const std::string k(knob);
+    if (k == "bs") g_path_bs = value != 0;
+    else if (k == "sub") g_path_sub = value != 0;
+    else if (k == "prune") g_path_prune = value != 0;
+    else if (k == "unit_width" && value >= -1 && value <= 1) g_path_unit_width = value;
+    else return RS_ERR_INVALID_ARG;
+    return RS_OK;
 }
 
 const char *rs_strerror(int code) {

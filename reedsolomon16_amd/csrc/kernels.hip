@@ -1023,14 +1023,10 @@ constexpr uint64_t kLdsMinGrid = 512;
 constexpr bool enc_acc_regs(int logm) { return logm % 2 == 0 && logm >= 4; }
 constexpr bool kLdsBranchFree = 1;  // lane-varying passes: branch-free multiplies
 
-// RS_UNIT_WIDTH=wide / narrow forces the per-launch unit-width choices below
-// (LDS tiles of 128 vs 64 bytes; GF(2^8) register units of 16 vs 4 bytes) so
-// the parity tests cover every variant at small sizes.  Testing only.
-int unit_width_override() {
-    const char *e = getenv("RS_UNIT_WIDTH");
-    if (!e) return -1;
-    return e[0] == 'n' ? 1 : e[0] == 'w' ? 0 : -1;
-}
+// rs_debug_set_path("unit_width", 0 / 1) forces the per-launch unit-width
+// choices below (LDS tiles of 128 vs 64 bytes; GF(2^8) register units of 16
+// vs 4 bytes) so the parity tests cover every variant at small sizes; -1 (the
+// default) keeps the automatic choice.  Testing only.
 bool pick_narrow(bool automatic) {
     const int o = unit_width_override();
     return o < 0 ? automatic : o == 1;
@@ -1267,8 +1263,8 @@ template <int LOGN> constexpr int rec_lds_threads() { return LOGN >= 10 ? 1024 :
 // n = 512..2048 with BSUB: the transforms in subfield coordinates wherever
 // every twiddle of a pass lies in GF(2^8) (rec_big_sub_passes; RecArgs::tw_*_sub).
 template <int LOGN> struct BigSub {
-    static constexpr int NI = LOGN == 11 ? 2 : 1;  // IFFT passes [NI, end) subfield
-    static constexpr int FEND = 4;                 // FFT passes [0, FEND) subfield
+    static constexpr int NI = big_sub_ifft_first(LOGN);  // IFFT passes [NI, end) subfield
+    static constexpr int FEND = big_sub_fft_end(LOGN);   // FFT passes [0, FEND) subfield
 };
 
 template <class F, class FT, int LOGN, bool BSUB = false>

@@ -48,6 +48,18 @@ struct EncodeArgs {
 };
 
 // Returns hipSuccess or the launch error.  logm in [0, 5].
+// Subfield passes of the n = 512..2048 LDS reconstruct (k_rec_lds BigSub):
+// the IFFT's radix-4 passes from big_sub_ifft_first(logn) on and the FFT's
+// passes before big_sub_fft_end(logn) run in GF(2^8)-subfield coordinates.
+// The host (codec.cpp upload_big_sub) checks every twiddle slot of exactly
+// these passes against the schedule, so both sides share these definitions.
+constexpr int big_sub_ifft_first(int logn) { return logn == 11 ? 2 : 1; }
+constexpr int big_sub_fft_end(int logn) { return (void)logn, 4; }
+
+// Test-only kernel-path overrides (rs_debug_set_path, codec.cpp): the LDS /
+// register unit width, -1 = automatic, 0 = wide, 1 = narrow.
+int unit_width_override();
+
 hipError_t launch_encode_reg(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 // Half-wave split encode (GF(2^16), logm 2..5, strided rows only: data.table ==
 // nullptr, and (k-1)*stride + shard_size < 2^32).  tw_ifft = nchunks images of

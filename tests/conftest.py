@@ -13,6 +13,16 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+@pytest.fixture
+def paths():
+    """rs_debug_set_path(knob, value): force a kernel path for one test; every
+    knob is back at its default afterwards."""
+    from reedsolomon16_amd import _capi
+
+    yield _capi.set_path
+    _capi.reset_paths()
+
+
 def _gpu_available() -> bool:
     try:
         import torch

@@ -143,6 +143,21 @@ def test_constructor_errors():
     assert rs.New16(1024, 300).encode_path == "multipass"
 
 
+def test_debug_set_path_knobs(paths):
+    """rs_debug_set_path: the test-only kernel-path overrides (no environment
+    variable reaches the product library)."""
+    paths("bs", 0)
+    assert rs.New16(128, 32).encode_path == "split16-m32"
+    paths("bs", 1)
+    assert rs.New16(128, 32).encode_path == "bs16-m32"
+    for knob, value in (("sub", 0), ("prune", 0), ("unit_width", 1), ("unit_width", 0), ("unit_width", -1)):
+        paths(knob, value)
+    with pytest.raises(ValueError):
+        paths("unit_width", 2)
+    with pytest.raises(ValueError):
+        paths("RS_BS", 0)
+
+
 def test_host_validation_errors_without_device():
     """Validation happens before any device work (Encode leopard16.go:116-135,
     reconstruct :390-430)."""

@@ -219,10 +219,10 @@ def test_gf8_reference_inversion_cache_random_sequences(torch, entry, S):
 
 @pytest.mark.parametrize("bits,k,p", [(16, 128, 32), (8, 128, 32), (16, 100, 28), (8, 10, 4)])
 @pytest.mark.parametrize("nerased", [1, 2, 3, 8])
-def test_pruned_fft_equals_unpruned_and_oracle(torch, monkeypatch, bits, k, p, nerased):
+def test_pruned_fft_equals_unpruned_and_oracle(torch, paths, bits, k, p, nerased):
     """The LDS reconstruct skips FFT groups whose rows are not revealed (the
     analog of errorBitfield, leopard16.go:1076-1252 / leopard8.go:1165-1273):
-    the rebuilt rows equal the unpruned run (RS_NO_PRUNE=1) and the oracle."""
+    the rebuilt rows equal the unpruned run (rs_debug_set_path("prune", 0)) and the oracle."""
     S = 4096 + 256
     rng = np.random.default_rng(k + p + nerased + bits)
     data = rng.integers(0, 256, (k, S), dtype=np.uint8)
@@ -235,7 +235,7 @@ def test_pruned_fft_equals_unpruned_and_oracle(torch, monkeypatch, bits, k, p, n
         mask[er] = True
         outs = []
         for noprune in ("0", "1"):
-            monkeypatch.setenv("RS_NO_PRUNE", noprune)
+            paths("prune", int(noprune != "1"))
             c = rs.ReedSolomon(k, p, bits)
             slab = torch.from_numpy(full.copy()).cuda()
             slab[torch.from_numpy(np.flatnonzero(mask)).cuda()] = 0

@@ -405,10 +405,10 @@ def test_host_pipeline_c3_pinned_matches_device(torch_dev):
 
 
 @pytest.mark.parametrize("k,p", [(128, 32), (100, 28), (10, 4), (300, 100), (700, 200), (1024, 256)])
-def test_reconstruct_subfield_equals_full_field(torch_dev, monkeypatch, k, p):
+def test_reconstruct_subfield_equals_full_field(torch_dev, paths, k, p):
     """The LDS reconstruct in GF(2^8)-subfield coordinates (every pass for
     n <= 256, all but the first passes of each transform at n = 512..2048:
-    kernels.hip BigSub) and the full-field table path (RS_NO_SUB=1) rebuild
+    kernels.hip BigSub) and the full-field table path (rs_debug_set_path("sub", 0)) rebuild
     identical bytes."""
     torch = torch_dev
     S = 4096 + 192
@@ -421,7 +421,7 @@ def test_reconstruct_subfield_equals_full_field(torch_dev, monkeypatch, k, p):
     present[np.random.default_rng(k).choice(k + p, p, replace=False)] = False
     out = []
     for nosub in ("0", "1"):
-        monkeypatch.setenv("RS_NO_SUB", nosub)
+        paths("sub", int(nosub != "1"))
         c = rs.New16(k, p)
         broken = full.clone()
         broken[torch.from_numpy(np.flatnonzero(~present)).cuda()] = 0
@@ -431,8 +431,8 @@ def test_reconstruct_subfield_equals_full_field(torch_dev, monkeypatch, k, p):
     assert torch.equal(out[0], full) and torch.equal(out[1], full)
 
 
-def test_bitsliced_equals_split_kernel(torch_dev, monkeypatch):
-    """C3 geometry: bit-sliced kernel (default) and the split perm kernel (RS_BS=0) agree."""
+def test_bitsliced_equals_split_kernel(torch_dev, paths):
+    """C3 geometry: bit-sliced kernel (default) and the split perm kernel (rs_debug_set_path("bs", 0)) agree."""
     torch = torch_dev
     k, p, S = 128, 32, 4096 * 4
     g = torch.Generator(device="cuda")
@@ -440,7 +440,7 @@ def test_bitsliced_equals_split_kernel(torch_dev, monkeypatch):
     base = torch.randint(0, 256, (k + p, S), dtype=torch.uint8, device="cuda", generator=g)
     outs = []
     for bs in ("1", "0"):
-        monkeypatch.setenv("RS_BS", bs)
+        paths("bs", int(bs))
         c = rs.New16(k, p)
         assert c.encode_path == ("bs16-m32" if bs == "1" else "split16-m32")
         slab = base.clone()
@@ -629,7 +629,7 @@ def test_device_encode_two_streams(torch_dev, bits, k, p, S, layout):
         assert np.array_equal(got, orc.encode(bits, k, p, datas[j])), f"stream {j}"
 
 
-# Unit-width variants (RS_UNIT_WIDTH forces the per-launch choice): the
+# Unit-width variants (rs_debug_set_path("unit_width") forces the per-launch choice): the
 # 64-byte and 128-byte LDS tiles of the LDS-resident encode / reconstruct
 # (both fields, both coordinate systems), and the 4- and 16-byte GF(2^8)
 # register units, at sizes the oracle finishes in seconds.
@@ -637,9 +637,9 @@ def test_device_encode_two_streams(torch_dev, bits, k, p, S, layout):
 @pytest.mark.parametrize("bits,k,p,S", [(8, 10, 4, 4096), (8, 100, 28, 4096 + 192), (16, 100, 28, 4096 + 192),
                                         (16, 70, 40, 2048), (8, 70, 40, 2048), (16, 128, 32, 4096 + 640),
                                         (16, 100, 100, 2048), (8, 100, 100, 2048), (16, 700, 200, 1024)])
-def test_unit_width_variants(monkeypatch, width, bits, k, p, S):
-    monkeypatch.setenv("RS_UNIT_WIDTH", width)
-    monkeypatch.setenv("RS_BS", "0")
+def test_unit_width_variants(paths, width, bits, k, p, S):
+    paths("unit_width", 1 if width == "narrow" else 0)
+    paths("bs", 0)
     rng = np.random.default_rng(k + p + S + bits)
     data = rand_data(rng, k, S)
     ref = orc.encode(bits, k, p, data)
@@ -649,7 +649,7 @@ def test_unit_width_variants(monkeypatch, width, bits, k, p, S):
     assert np.array_equal(np.stack(shards[k:]), ref), c.encode_path
     full = [data[i] for i in range(k)] + [ref[i] for i in range(p)]
     for nosub in (["0", "1"] if bits == 16 else ["0"]):
-        monkeypatch.setenv("RS_NO_SUB", nosub)
+        paths("sub", int(nosub != "1"))
         c2 = rs.ReedSolomon(k, p, bits)
         er = set(rng.choice(k + p, p, replace=False).tolist())
         sh = [None if i in er else full[i].copy() for i in range(k + p)]
@@ -786,9 +786,9 @@ def test_n256_reconstruct(k, p, S):
             assert np.array_equal(sh[i], ref[i]), f"shard {i} vs oracle"
 
 
-def test_n256_reconstruct_full_field(monkeypatch):
-    """n = 256 reconstruct with transforms outside subfield coordinates (RS_NO_SUB=1)."""
-    monkeypatch.setenv("RS_NO_SUB", "1")
+def test_n256_reconstruct_full_field(paths):
+    """n = 256 reconstruct with transforms outside subfield coordinates (rs_debug_set_path("sub", 0))."""
+    paths("sub", 0)
     k, p, S = 128, 32, 1024
     rng = np.random.default_rng(77)
     data = rand_data(rng, k, S)
@@ -969,16 +969,16 @@ def test_verify_and_reconstruct_async_stream_of_blocks(k, p, S):
 
 
 @pytest.mark.parametrize("k,p,S", [(1024, 256, 1024), (300, 200, 512), (100, 40, 256), (1000, 129, 128)])
-def test_lds_encode_subfield_chunk_passes(torch_dev, monkeypatch, k, p, S):
+def test_lds_encode_subfield_chunk_passes(torch_dev, paths, k, p, S):
     """k_enc_lds with the chunk IFFTs in subfield coordinates from their first
     all-subfield pass on (EncodeArgs::tw_ifft_sub, default) and the full-field
-    chunk IFFTs (RS_NO_SUB=1) both give the oracle's parity, and verify it."""
+    chunk IFFTs (rs_debug_set_path("sub", 0)) both give the oracle's parity, and verify it."""
     torch = torch_dev
     rng = np.random.default_rng(k + p + S)
     data = rand_data(rng, k, S)
     ref = orc.encode(16, k, p, data)
     for nosub in ("0", "1"):
-        monkeypatch.setenv("RS_NO_SUB", nosub)
+        paths("sub", int(nosub != "1"))
         c = rs.New16(k, p)
         assert c.encode_path.startswith("lds-m")
         slab = torch.zeros((2, k + p, S), dtype=torch.uint8, device="cuda")
