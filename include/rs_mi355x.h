@@ -157,10 +157,11 @@ int rs_set_host_segment(rs_codec *codec, size_t bytes);
  * parity erasures unless recoverAll, and stores them under the bitfield after
  * prepare(); a later call whose erasures differ only in ways the key does not
  * see then reuses errLocs computed for another pattern, and rebuilds wrong
- * data.  By default (on = 0) the engine keys its caches on the exact pattern
- * and always rebuilds the right data; on = 1 reproduces the reference's output
- * call for call, stale results included.  Switching clears the cache, as a
- * fresh newFF8 would.  No effect on GF(2^16) codecs or above 64 shards. */
+ * data.  By default (on = 1) the engine keeps this cache as the reference
+ * does, per codec, and reproduces the reference's output call for call, stale
+ * results included; on = 0 keys the locators on the exact erasure pattern and
+ * always rebuilds the right data.  Each call of this function clears the cache, as a fresh
+ * newFF8 would.  No effect on GF(2^16) codecs or above 64 shards. */
 int rs_set_reference_inversion_cache(rs_codec *codec, int on);
 /* Pinned, 64-byte-aligned host memory: AllocAligned (unsafe.go:17-41) for
  * shards that are to cross PCIe at full rate. */

@@ -229,6 +229,7 @@ class ReedSolomon:
         self._L = L
         self.device = device
         self._arena = _PinnedArena()
+        self._ref_inv = True  # rs_set_reference_inversion_cache default
 
     def close(self):
         if getattr(self, "_h", None):
@@ -282,9 +283,16 @@ class ReedSolomon:
     def set_reference_inversion_cache(self, on: bool) -> None:
         """GF(2^8): reproduce leopard8.go:508-555's inversion cache call for
         call, including the stale errLocs it hands out when two erasure
-        patterns share its key (include/rs_mi355x.h).  Off by default: the
-        engine keys its caches on the exact pattern."""
+        patterns share its key (include/rs_mi355x.h).  On by default, as the
+        reference keeps it; off keys the locators on the exact pattern.
+        Clears the cache, as a fresh newFF8 would."""
         _check(self._L.rs_set_reference_inversion_cache(self._h, 1 if on else 0))
+        self._ref_inv = bool(on)
+
+    def reset_inversion_cache(self) -> None:
+        """Empty the GF(2^8) inversion cache, keeping the mode: the state of a
+        fresh newFF8 (the reference's stream wrappers build one per call)."""
+        self.set_reference_inversion_cache(self._ref_inv)
 
     # ---------------- host-memory operations (Go [][]byte semantics)
     def encode(self, shards: list) -> None:

@@ -186,14 +186,14 @@ struct HpEncoder {
     // an empty range.  Lanes whose block lies past the row end read bytes of
     // the next row; their results are never stored.
     template <int I0, int I1>
-    __device__ __forceinline__ void stage(const Loc &L, int c, bool idle = false) {
+    __device__ __forceinline__ void stage(const Loc &L, int c) {
         const uint32_t range = L.live ? a.span : 0u;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(a.data + (L.live ? (uint64_t)L.stripe * a.stripe_stride : 0)), 0, (int)range, 0x00020000);
         // lane part of the offset (block, half); opaque so that the compiler
         // does not precompute every chunk's offsets
-        uint32_t voff = idle ? 0u : (uint32_t)L.ct * TILE + (uint32_t)blk * 64 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
-        const uint32_t qs = idle ? 0u : 16u;
+        uint32_t voff = (uint32_t)L.ct * TILE + (uint32_t)blk * 64 + (uint32_t)(HR * h) * (uint32_t)a.row_stride;
+        constexpr uint32_t QS = 16;
         asm volatile("" : "+v"(voff));
         // the loads issue at raised wave priority, ahead of the other waves'
         // VALU: one stripe per launch 0.524-0.527 -> 0.547-0.552 of the
@@ -203,10 +203,10 @@ struct HpEncoder {
 #pragma unroll
         for (int i = I0; i < I1; i++) {
             // wave-uniform row of the h = 0 lanes (rows >= k are out of range: zeros)
-            const uint32_t soff = idle ? 0u : (uint32_t)(M * c + RW * w + i) * (uint32_t)a.row_stride;
+            const uint32_t soff = (uint32_t)(M * c + RW * w + i) * (uint32_t)a.row_stride;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * qs, soff, 0);
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * QS, soff, 0);
                 uint32_t *d = q < 2 ? &St[i][q * 4] : &St[HR + i][(q - 2) * 4];
                 d[0] = x[0], d[1] = x[1], d[2] = x[2], d[3] = x[3];
             }
@@ -227,16 +227,11 @@ struct HpEncoder {
         });
     }
 
-    // Next chunk's rows i in [I0, I1): chunk C + 1 of this tile.  The last
-    // chunk issues nothing: a workgroup runs one tile (launch_hp_t), so there
-    // is no next tile to fetch for (a scalar branch on the wave-uniform nch).
-    // The last chunk's loads still issue (a branch around them spills 46
-    // VGPRs: the staged registers would have to survive both paths), but all
-    // of their lanes read one 16-byte word at the stripe's start, so they cost
-    // one coalesced request each instead of 32 cache lines of the row pattern.
+    // Next chunk's rows i in [I0, I1): chunk C + 1 of this tile, or chunk 0 of the next tile.
     template <int C, int I0, int I1>
-    __device__ __forceinline__ void prefetch(const Loc &cur) {
-        stage<I0, I1>(cur, C + 1, C + 1 >= nch);
+    __device__ __forceinline__ void prefetch(const Loc &cur, const Loc &nxt) {
+        const bool more = C + 1 < nch;  // wave-uniform: one load sequence, no branch
+        stage<I0, I1>(more ? cur : nxt, more ? C + 1 : 0);
     }
 
     // The next chunk's loads go out in two halves so that (m = 32) at most
@@ -247,7 +242,7 @@ struct HpEncoder {
     // (Issuing all of them at the chunk start, with 192 VGPRs of data live,
     // spilled to scratch: +8 % HBM traffic.)
     template <int C>
-    __device__ __forceinline__ void chunk(const Loc &cur) {
+    __device__ __forceinline__ void chunk(const Loc &cur, const Loc &nxt) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < RW; i++)
@@ -266,14 +261,14 @@ struct HpEncoder {
 #pragma unroll
             for (int q = 0; q < 8; q++) asm volatile("" : "+v"(R[i][q])::"memory");
         __builtin_amdgcn_sched_barrier(0);
-        prefetch<C, 0, PF1>(cur);
+        prefetch<C, 0, PF1>(cur, nxt);
         __builtin_amdgcn_sched_barrier(0);
         dispatch<4>(w, [&](auto W) { phase1<C, decltype(W)::value>(); });
         lds_barrier();  // every wave has read the previous image
 #pragma unroll
         for (int j = 0; j < RW; j++) hp_put(lbase, RW * w + j, R[j]);
         lds_barrier();
-        prefetch<C, PF1, HR>(cur);
+        prefetch<C, PF1, HR>(cur, nxt);
         __builtin_amdgcn_sched_barrier(0);
         // IFFT layers r(LR), r(LR+1), one coset at a time
 #pragma unroll
@@ -301,8 +296,8 @@ struct HpEncoder {
     // chunks is never fetched).  Chunk 0 unconditionally: with a branch
     // around it too, the allocator spilled 11-14 VGPRs.
     template <int... Cs>
-    __device__ __forceinline__ void chunks(const Loc &cur, std::integer_sequence<int, Cs...>) {
-        ((Cs == 0 || Cs < nch ? (chunk<Cs>(cur), 0) : 0), ...);
+    __device__ __forceinline__ void chunks(const Loc &cur, const Loc &nxt, std::integer_sequence<int, Cs...>) {
+        ((Cs == 0 || Cs < nch ? (chunk<Cs>(cur, nxt), 0) : 0), ...);
     }
 
     // FFT layers r(LR-1) .. r0 on rows RW*W + j.
@@ -318,12 +313,13 @@ struct HpEncoder {
         });
     }
 
-    // One tile per workgroup (launch_hp_t's grid is the tile count).
     __device__ __forceinline__ void run() {
-        const Loc cur = locate(blockIdx.x);
+        int tile = blockIdx.x;
+        Loc cur = locate(tile);
         stage<0, HR>(cur, 0);
-        {
-            chunks(cur, std::make_integer_sequence<int, NCH>{});
+        for (; tile < a.ntiles; tile += gridDim.x) {
+            const Loc nxt = locate(tile + (int)gridDim.x);
+            chunks(cur, nxt, std::make_integer_sequence<int, NCH>{});
             // FFT layers r(LR+1), r(LR) in A's layout
 #pragma unroll
             for (int u = 0; u < U; u++) {
@@ -383,6 +379,7 @@ struct HpEncoder {
                     __hip_atomic_load(a.mismatch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
                     __hip_atomic_store(a.mismatch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            cur = nxt;
         }
     }
 };

@@ -209,9 +209,10 @@ struct rs_codec {
     std::list<std::pair<std::vector<uint8_t>, std::vector<uint32_t>>> el_cache;
     // rs_set_reference_inversion_cache: the GF(2^8) inversion cache exactly as
     // leopard8.go:508-555 keys it (raw erasure bits on lookup, bits after
-    // prepare() on store), for callers that need the reference's output on
-    // every call sequence; off by default
-    bool ref_inv = false;
+    // prepare() on store), so the output is the reference's on every call
+    // sequence; on by default (a drop-in returns the reference's bytes), off
+    // keys the locators on the exact pattern
+    bool ref_inv = true;
     std::map<std::array<uint64_t, 4>, std::vector<uint32_t>> ref_inv_cache;
 
     // host-resident pipeline (rs_encode / rs_verify / rs_reconstruct): copy-in,

@@ -305,11 +305,20 @@ class _StreamCodec:
             if inputs[i] is not None and outputs[i] is not None:
                 raise ErrReconstructMismatch("a shard cannot be both an input and an output")
 
+    def _fresh_codec(self) -> None:
+        """Every rsFF8 Stream* call builds its own rsStreamFF8 and newFF8
+        (reedsolomon.go:132,147,169), whose inversion cache starts empty
+        (leopard8.go:67-71): clear the engine's before each stream operation."""
+        reset = getattr(self.rs, "reset_inversion_cache", None)
+        if self.FIELD == 8 and reset is not None:
+            reset()
+
     def reconstruct_data(self, inputs: Sequence, outputs: Sequence) -> None:
         """rsStream16.reconstructData (streaming16.go:471-632) /
         rsStreamFF8.reconstructData (streaming8.go:609-766): rebuilds only
         missing data shards; a nil parity input is fed as a zero shard."""
         self._check_io(inputs, outputs)
+        self._fresh_codec()
         missing = [i < self.k and inputs[i] is None and outputs[i] is not None for i in range(self.total)]
         self._reconstruct_loop(inputs, outputs, missing, recover_all=False, data_loop=True)
 
@@ -411,6 +420,7 @@ class StreamEncoder8(_StreamCodec):
         output receives zeros, ``size`` bytes per data shard and
         ``ceil64(size)`` per parity shard (:586-604)."""
         self._check_io(inputs, outputs)
+        self._fresh_codec()
         recover_all = any(outputs[i] is not None for i in range(self.k, self.total))  # :459-467
         bufs = self._buffers()
         blk, read = 0, 0

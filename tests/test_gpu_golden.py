@@ -12,12 +12,11 @@
   "first 32 data shards", parity-only, data-only), at a window size the
   oracle finishes in seconds;
 * the GF(2^8) inversion-cache sequence of leopard8.go:508-555 (a cached
-  error-locator vector reused for a different parity-erasure pattern): the
-  engine keys its cache on the exact pattern and returns the correct shard,
-  where the reference (oracle) returns the stale result.  INTEGRATION.md
-  states this divergence; rs_set_reference_inversion_cache(1) reproduces the
-  reference's results call for call (random call sequences, host and device
-  entry points, against the oracle).
+  error-locator vector reused for a different parity-erasure pattern): by
+  default the engine keeps the reference's cache and returns the reference's
+  (stale) result, call for call against the oracle on random call sequences
+  through the host and device entry points; rs_set_reference_inversion_cache(0)
+  keys the cache on the exact pattern and returns the correct shard.
 """
 import os
 
@@ -60,6 +59,10 @@ def test_golden_replay_host(name):
     assert c.verify(shards)
     full = [g["data"][i] for i in range(k)] + [g["parity"][i] for i in range(p)]
     for er in g["erasures"]:
+        # a codec per mask, as a fresh reference encoder would be: the GF(2^8)
+        # inversion cache (leopard8.go:508-555, kept by default) does not carry
+        # one mask's locators into another's
+        c = rs.ReedSolomon(k, p, bits)
         sh = [None if er[i] else full[i].copy() for i in range(k + p)]
         c.reconstruct(sh)
         for i in range(k + p):
@@ -83,6 +86,7 @@ def test_golden_replay_device(torch, name):
     assert np.array_equal(slab[k:].cpu().numpy(), g["parity"])
     full = slab.clone()
     for er in g["erasures"]:
+        c = rs.ReedSolomon(k, p, bits)  # a codec per mask (see test_golden_replay_host)
         present = er == 0
         broken = full.clone()
         broken[torch.from_numpy(np.flatnonzero(er)).cuda()] = 0
@@ -128,13 +132,14 @@ def test_reconstruct_dev_equals_oracle(torch, pattern, recover_all):
             assert np.array_equal(got[i], ref[i]), (pattern, i)
 
 
-def test_gf8_inversion_cache_sequence():
+def test_gf8_inversion_cache_sequence_exact_mode():
     """leopard8.go:508-555 with total <= 64 (cache on): ReconstructData with
     data 0 + parity 0 erased, then with data 0 only.  The reference keys its
     cache on the data-erasure bitmap alone (parity bits only when recoverAll),
     so its second call reuses the first call's error locators and returns a
-    wrong shard 0 (the oracle reproduces it).  The engine's cache key is the
-    exact pattern: shard 0 comes back correct."""
+    wrong shard 0 (the oracle reproduces it).  With
+    rs_set_reference_inversion_cache(0) the engine keys its cache on the exact
+    pattern: shard 0 comes back correct."""
     k, p, S = 10, 4, 64
     data = np.random.default_rng(2).integers(0, 256, (k, S), dtype=np.uint8)
     par = orc.encode(8, k, p, data)
@@ -144,24 +149,25 @@ def test_gf8_inversion_cache_sequence():
     e, stale = o.reconstruct([None if i == 0 else full[i].copy() for i in range(k + p)], False)
     assert e == 0 and not np.array_equal(stale[0], full[0])  # the reference's result
     c = rs.New8(k, p)
+    c.set_reference_inversion_cache(False)
     sh = [None if i in (0, k) else full[i].copy() for i in range(k + p)]
     c.reconstruct_data(sh)
     assert np.array_equal(sh[0], full[0])
     sh = [None if i == 0 else full[i].copy() for i in range(k + p)]
     c.reconstruct_data(sh)
-    assert np.array_equal(sh[0], full[0])  # the engine's (correct) result
+    assert np.array_equal(sh[0], full[0])  # the exact mode's (correct) result
 
 
-def test_gf8_inversion_cache_sequence_reference_mode():
-    """rs_set_reference_inversion_cache(1): the same sequence returns the
-    reference's stale shard 0, byte for byte the oracle's."""
+def test_gf8_inversion_cache_sequence_default_is_reference():
+    """By default the same sequence returns the reference's stale shard 0,
+    byte for byte the oracle's; reset_inversion_cache() (a fresh newFF8)
+    forgets it."""
     k, p, S = 10, 4, 64
     data = np.random.default_rng(2).integers(0, 256, (k, S), dtype=np.uint8)
     par = orc.encode(8, k, p, data)
     full = [data[i] for i in range(k)] + [par[i] for i in range(p)]
     o = orc.Oracle(8, k, p)
     c = rs.New8(k, p)
-    c.set_reference_inversion_cache(True)
     for erased in ((0, k), (0,)):
         e, ref = o.reconstruct([None if i in erased else full[i].copy() for i in range(k + p)], False)
         assert e == 0
@@ -169,6 +175,10 @@ def test_gf8_inversion_cache_sequence_reference_mode():
         c.reconstruct_data(sh)
         assert np.array_equal(sh[0], ref[0])
     assert not np.array_equal(sh[0], full[0])  # the stale result, as the reference returns it
+    c.reset_inversion_cache()
+    sh = [None if i == 0 else full[i].copy() for i in range(k + p)]
+    c.reconstruct_data(sh)
+    assert np.array_equal(sh[0], full[0])
 
 
 @pytest.mark.parametrize("entry", ["host", "device"])
@@ -177,7 +187,7 @@ def test_gf8_reference_inversion_cache_random_sequences(torch, entry, S):
     """60 reconstructs of one GF(2^8) codec (40 + 16: total <= 64, so the
     reference caches) over erasure sets drawn from a few shards, with random
     recoverAll, in reference mode: every rebuilt shard equals the oracle's on
-    the same call sequence.  At S = 2048 one-to-four erasures take the
+    the same call sequence (the default mode).  At S = 2048 one-to-four erasures take the
     reference's useBits branch (leopard8.go:474), whose store key is the
     prepared bitfield (:1192-1199), so a later pattern with both bits of a
     pair erased reuses errLocs computed for one of them; at S = 64 only the
@@ -188,8 +198,7 @@ def test_gf8_reference_inversion_cache_random_sequences(torch, entry, S):
     par = orc.encode(8, k, p, data)
     full = np.concatenate([data, par])
     o = orc.Oracle(8, k, p)
-    c = rs.New8(k, p)
-    c.set_reference_inversion_cache(True)
+    c = rs.New8(k, p)  # reference mode is the default
     pool = [0, 1, 2, 3, 6, 7, k, k + 1, k + 5]
     stale = 0
     for _ in range(60):

@@ -41,6 +41,10 @@ class OracleTicketCodec:
         self.orc = Oracle(bits, k, p)
         self.calls = []
 
+    def reset_inversion_cache(self):
+        """A fresh newFF8's empty inversion cache (stream.py _fresh_codec)."""
+        self.orc = Oracle(self.orc.bits, self.k, self.p)
+
     def alloc_aligned(self, each, shards=None, pinned=False):
         n = self.total if shards is None else shards
         slab = np.full(each * n, 0xA5, np.uint8)  # not zero: the mirror must not rely on fresh memory
