@@ -630,53 +630,59 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
                 p3b = -1;
             }
         }
-        if (early_p1) {
-            // ---- early phase 1 of tile tn (registers only); a first unit parks in V[8..15]
-            // The early waves' chain is the critical path: it issues ahead of
-            // the phase-2 / phase-3 waves sharing its SIMD (C4 x 16 1692 ->
-            // 1637 us, one stripe 124 -> 121 us; raising the phase-3 waves too
-            // gained nothing, profiles/r03_c4_prio_ab.txt).
-            __builtin_amdgcn_s_setprio(3);
-            set_tile(tn);
-            const int n1 = p1b >= 0 ? 2 : 1;
-            // (loading unit b's rows into V[8..15] up front measured slower:
-            // 1950 vs 1694 us per 16 C4 stripes)
+        // Two slots, one copy of the phase-1 code: slot 0 runs the early
+        // waves' phase 1 of tile tn (before phase 2), slot 1 phases 2 and 3 of
+        // tile t and then the late waves' phase 1 of tile tn.  Two call sites
+        // of phase1() put its code (scale-in, IFFT layers 0-3 of every unit)
+        // into the kernel twice: 112 KB against a 64 KB instruction cache
+        // (one instruction-cache-sized build measured 9 % faster).
 #pragma nounroll
-            for (int s = 0; s < n1; s++) {  // one copy of the phase-1 code
-                if (s) d.park_swap();
-                d.phase1(s ? p1b : p1a, s == 0 && cur ? 2 : 0);
-            }
-            __builtin_amdgcn_s_setprio(0);
-        }
-        if (cur) {
-            // ---- phase 2: Y = B_F (I + H) B_I u + Lo u (B layout)
-            if (!early)
-                d.phase2();
-            if (!early_p1) lds_barrier();  // every wave has read u
-            if (!early) {
-                int wt = w;
-                asm volatile("" : "+s"(wt));
+        for (int slot = 0; slot < 2; slot++) {
+            if (slot == 1 && cur) {
+                // ---- phase 2: Y = B_F (I + H) B_I u + Lo u (B layout)
+                if (!early)
+                    d.phase2();
+                if (!early_p1) lds_barrier();  // every wave has read u
+                if (!early) {
+                    int wt = w;
+                    asm volatile("" : "+s"(wt));
 #pragma unroll
-                for (int q = 0; q < Dec<STRIDED>::NQ; q++) d.img_put(2 * wt + 16 * q, d.V[q]);
-            }
-            if (!early_p1) lds_barrier();  // Y is in the image
-            if (p3a >= 0) {
-                // ---- phase 3 of tile t, one unit at a time (each read from the
-                // image before the barrier below frees it)
-                set_tile(t);
-                const int n3 = p3b >= 0 ? 2 : 1;
+                    for (int q = 0; q < Dec<STRIDED>::NQ; q++) d.img_put(2 * wt + 16 * q, d.V[q]);
+                }
+                if (!early_p1) lds_barrier();  // Y is in the image
+                if (p3a >= 0) {
+                    // ---- phase 3 of tile t, one unit at a time (each read from the
+                    // image before the barrier below frees it)
+                    set_tile(t);
+                    const int n3 = p3b >= 0 ? 2 : 1;
 #pragma nounroll
-                for (int s = 0; s < n3; s++) {
-                    const int u = s ? p3b : p3a;
-                    d.template unit_get<0>(u);
-                    d.phase3(u);
+                    for (int s = 0; s < n3; s++) {
+                        const int u = s ? p3b : p3a;
+                        d.template unit_get<0>(u);
+                        d.phase3(u);
+                    }
                 }
             }
-        }
-        if (!early && more && p1a >= 0) {
-            // ---- late phase 1 of tile tn (registers only)
-            set_tile(tn);
-            d.phase1(p1a);
+            // ---- phase 1 of tile tn (registers only): the early waves in slot 0,
+            // a first unit parked in V[8..15]; the late waves in slot 1
+            const bool run_p1 = slot == 0 ? early_p1 : !early && more && p1a >= 0;
+            if (run_p1) {
+                // The early waves' chain is the critical path: it issues ahead of
+                // the phase-2 / phase-3 waves sharing its SIMD (C4 x 16 1692 ->
+                // 1637 us, one stripe 124 -> 121 us; raising the phase-3 waves too
+                // gained nothing, profiles/r03_c4_prio_ab.txt).
+                if (slot == 0) __builtin_amdgcn_s_setprio(3);
+                set_tile(tn);
+                const int n1 = slot == 0 && p1b >= 0 ? 2 : 1;
+                // (loading unit b's rows into V[8..15] up front measured slower:
+                // 1950 vs 1694 us per 16 C4 stripes)
+#pragma nounroll
+                for (int s = 0; s < n1; s++) {
+                    if (s) d.park_swap();
+                    d.phase1(s ? p1b : p1a, slot == 0 && s == 0 && cur ? 2 : 0);
+                }
+                __builtin_amdgcn_s_setprio(0);
+            }
         }
         if (!more) break;
         lds_barrier();  // the image is free for phase 1 of tile tn
