@@ -313,12 +313,16 @@ struct HpEncoder {
         });
     }
 
+    // Workgroup b runs tiles t0 + i * step, i < tpw (launch_hp_t): t0 =
+    // (b / step) * step * tpw + b % step, so the tiles of the grid are each run once.
     __device__ __forceinline__ void run() {
-        int tile = blockIdx.x;
+        const int b = blockIdx.x, step = a.tile_step;
+        int tile = (b / step) * step * a.tpw + b % step;
+        const int tend = min(a.ntiles, tile + step * a.tpw);
         Loc cur = locate(tile);
         stage<0, HR>(cur, 0);
-        for (; tile < a.ntiles; tile += gridDim.x) {
-            const Loc nxt = locate(tile + (int)gridDim.x);
+        for (; tile < tend; tile += step) {
+            const Loc nxt = locate(tile + step < tend ? tile + step : a.ntiles);
             chunks(cur, nxt, std::make_integer_sequence<int, NCH>{});
             // FFT layers r(LR+1), r(LR) in A's layout
 #pragma unroll
@@ -406,13 +410,30 @@ hipError_t launch_hp_t(bool verify, BsArgs a, int cus, hipStream_t s) {
     a.ntiles = a.tiles_per_stripe * a.nstripes;
     a.span = (uint32_t)((uint64_t)(a.k - 1) * a.row_stride + a.S);
     a.pspan = (uint32_t)((uint64_t)(a.p - 1) * a.row_stride + a.S);
-    // One tile per workgroup: the hardware starts a new workgroup wherever
-    // one finishes, so the loads of starting tiles overlap the stores of
-    // finishing ones without the persistent grid's lockstep (same-box A/B,
-    // 128 C3 stripes: 4.39 -> 4.25 ms, 0.611 -> 0.631 of the HBM roofline,
-    // profiles/r03_c3_grid_ab.txt).
-    const int grid = a.ntiles;
-    (void)cus;
+    // Tiles per workgroup: workgroup b runs tiles t0, t0 + step, ... (run()),
+    // and each tile's last chunk prefetches the next tile's first (HpEncoder::
+    // prefetch), so only its first tile pays the load latency with nothing to
+    // overlap.  A fully persistent grid (one generation of workgroups) ran in
+    // lockstep and lost (round 3: 0.611 against 0.631 for one tile per
+    // workgroup, profiles/r03_c3_grid_ab.txt).  Round 5 (profiles/
+    // r05_c3_tiles_per_wg.txt): four tiles per workgroup, a grid size apart,
+    // take C3 launches of 224-512 full-row stripes from 0.65 to 0.69-0.71 on
+    // five of six boxes (one lost 0.01); adjacent tiles or a one- to
+    // sixteen-stripe distance lose (0.64-0.667).  Launches under ~200 tiles
+    // per workgroup slot (<= 192 full-row stripes, byte-range slices of 256
+    // stripes) gain little or lose on some boxes, so they keep one tile per
+    // workgroup.
+    const int slots = std::max(cus, 1) * kHpWgPerCu<LOGM>;
+    int tpw = hp_tiles_override();
+    if (tpw <= 0) tpw = a.ntiles >= 224 * slots ? 4 : 1;
+    int step = hp_step_override();
+    if (step <= 0) step = (a.ntiles + tpw - 1) / tpw;
+    step = std::min(step, a.ntiles);
+    // workgroups: full blocks of step * tpw tiles, then the remainder
+    const int blocks = a.ntiles / (step * tpw), rem = a.ntiles - blocks * step * tpw;
+    const int grid = blocks * step + std::min(rem, step);
+    a.tpw = tpw;
+    a.tile_step = step;
     if (verify) hipLaunchKernelGGL((k_encode_hp<LOGM, true>), dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_encode_hp<LOGM, false>), dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();

@@ -341,12 +341,14 @@ int upload_split(rs_codec *c) {
 // select (the bit-sliced encode off, the transforms in full-field coordinates,
 // the reconstruct FFT unpruned, the narrow / wide LDS units) on the same small
 // inputs.  Process-wide; read when a codec is created (bs) or at each launch.
-std::atomic<int> g_path_bs{1}, g_path_sub{1}, g_path_prune{1}, g_path_unit_width{-1};
+std::atomic<int> g_path_bs{1}, g_path_sub{1}, g_path_prune{1}, g_path_unit_width{-1}, g_path_hp_tiles{0}, g_path_hp_step{0};
 bool bs_enabled() { return g_path_bs.load(std::memory_order_relaxed) != 0; }
 bool sub_enabled() { return g_path_sub.load(std::memory_order_relaxed) != 0; }
 bool prune_enabled() { return g_path_prune.load(std::memory_order_relaxed) != 0; }
 }  // namespace
 int rs::unit_width_override() { return g_path_unit_width.load(std::memory_order_relaxed); }
+int rs::hp_tiles_override() { return g_path_hp_tiles.load(std::memory_order_relaxed); }
+int rs::hp_step_override() { return g_path_hp_step.load(std::memory_order_relaxed); }
 namespace {
 
 // Host half of the encode plan (no device calls): twiddle schedule and panic check.
@@ -2142,6 +2144,8 @@ int rs_debug_set_path(const char *knob, int value) {
     else if (k == "sub") g_path_sub = value != 0;
     else if (k == "prune") g_path_prune = value != 0;
     else if (k == "unit_width" && value >= -1 && value <= 1) g_path_unit_width = value;
+    else if (k == "hp_tiles" && value >= 0 && value <= 64) g_path_hp_tiles = value;
+    else if (k == "hp_step" && value >= 0) g_path_hp_step = value;
     else return RS_ERR_INVALID_ARG;
     return RS_OK;
 }

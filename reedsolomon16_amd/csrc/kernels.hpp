@@ -59,6 +59,10 @@ constexpr int big_sub_fft_end(int logn) { return (void)logn, 4; }
 // Test-only kernel-path overrides (rs_debug_set_path, codec.cpp): the LDS /
 // register unit width, -1 = automatic, 0 = wide, 1 = narrow.
 int unit_width_override();
+// The bit-sliced encode's tiles per workgroup: 0 = automatic, n >= 1 forces n;
+// and the distance in tiles between a workgroup's tiles, 0 = the grid size.
+int hp_tiles_override();
+int hp_step_override();
 
 hipError_t launch_encode_reg(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 // Half-wave split encode (GF(2^16), logm 2..5, strided rows only: data.table ==
@@ -152,6 +156,7 @@ struct BsArgs {
     uint64_t row_stride, stripe_stride, S;
     int k, p, nstripes;
     int tiles_per_stripe, ntiles;  // set by the launcher
+    int tpw, tile_step;            // set by the launcher: tiles per workgroup, tile distance between them
     uint32_t span, pspan;          // set by the launcher: (k-1)*row_stride + S, (p-1)*row_stride + S
     int *mismatch;          // verify
 };

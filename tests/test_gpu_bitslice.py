@@ -52,6 +52,31 @@ def test_bs_batch_matches_oracle(torch, k, p, S, n):
         assert np.array_equal(slab[j, k:].cpu().numpy(), orc.encode(16, k, p, datas[j])), f"stripe {j}"
 
 
+@pytest.mark.parametrize("tiles,step", [(2, 0), (3, 0), (4, 0), (4, 7), (3, 64), (8, 1), (5, 1000)])
+@pytest.mark.parametrize("k,p,S,n", [(128, 32, 2048 * 20 + 64, 6), (100, 17, 2048 * 9 + 320, 5), (64, 16, 2048 * 33, 4)])
+def test_bs_tiles_per_workgroup(torch, paths, tiles, step, k, p, S, n):
+    """Several tiles per workgroup (launch_hp_t): workgroup b runs tiles
+    t0 + i * step with the next tile's first chunk prefetched during the last
+    chunk of the current one; every (tiles, step), the ragged last block of
+    the grid included, gives the oracle's parity and verifies."""
+    paths("hp_tiles", tiles)
+    paths("hp_step", step)
+    rng = np.random.default_rng(tiles * 31 + step + k + S)
+    datas = [rng.integers(0, 256, (k, S), dtype=np.uint8) for _ in range(n)]
+    slab = torch.zeros((n, k + p, S), dtype=torch.uint8, device="cuda")
+    for j in range(n):
+        slab[j, :k] = torch.from_numpy(datas[j]).cuda()
+    c = rs.New16(k, p)
+    assert c.encode_path == path(p)
+    c.encode_dev_batch(slab)
+    torch.cuda.synchronize()
+    for j in range(n):
+        assert np.array_equal(slab[j, k:].cpu().numpy(), orc.encode(16, k, p, datas[j])), f"stripe {j}"
+    assert c.verify_dev_batch(slab)
+    slab[n - 1, k + p - 1, S - 1] ^= 1
+    assert not c.verify_dev_batch(slab)
+
+
 @pytest.mark.parametrize("k,p", [(128, 32), (64, 16)])
 def test_bs_special_inputs(torch, k, p):
     """All-zero, all-0xFF and single-symbol impulses in every chunk."""
