@@ -16,14 +16,20 @@ timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke(); print("smok
 rc=$?; echo "smoke rc=$rc"; tail -2 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py $BARGS > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu --no-single --no-unpadded --no-other $BARGS > $OUT/trace_bench.json 2> $OUT/trace.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu --no-single --no-unpadded --no-other --no-host $BARGS > $OUT/trace_bench.json 2> $OUT/trace.err
 rc=$?; echo "trace rc=$rc"; cat $OUT/trace_bench.json; [ $rc -eq 0 ] || exit $rc
+# per-shape kernel traces of the other workloads (one launch shape per run, so
+# no averages mix): C4 x 16 stripes, C2 one stripe and x 16, C5 x 32, C5 repair x 8
+for cfg in C4x16 C2 C2x16 C5b32 C5rb8; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$cfg -o run -- python3 scripts/time_ops.py --configs $cfg --iters 20 > $OUT/trace_$cfg.json 2> $OUT/trace_$cfg.err
+  rc=$?; echo "trace $cfg rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o run -- python3 bench.py --no-cpu --no-single --no-unpadded --no-other --steps 50 --warmup 5 > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o run -- python3 bench.py --no-cpu --no-single --no-unpadded --no-other --no-host --steps 50 --warmup 5 > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
   # the launch shape of each rank of an N-GPU byte-range run (bench.py --slice-of N)
   for n in 2 4 8; do
-    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${c}_s$n -o run -- python3 bench.py --slice-of $n --no-cpu --no-single --no-unpadded --no-other --steps 50 --warmup 5 > $OUT/pmc_${c}_s$n.json 2> $OUT/pmc_${c}_s$n.err
+    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${c}_s$n -o run -- python3 bench.py --slice-of $n --no-cpu --no-single --no-unpadded --no-other --no-host --steps 50 --warmup 5 > $OUT/pmc_${c}_s$n.json 2> $OUT/pmc_${c}_s$n.err
     rc=$?; echo "pmc $c slice $n rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
 done
