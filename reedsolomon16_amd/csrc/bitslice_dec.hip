@@ -542,22 +542,35 @@ struct Dec {
         if (u & 1) below += __builtin_popcount(word & 0xFFFFu);
         const int j_hi = below - below_m, j_lo = total - below_m + below;
         const uint32_t off = lane_off();
+        // The unit's byte-form rows go to its own 16 image rows, which no other
+        // wave reads between this wave's unit_get and the image-free barrier;
+        // one rolled loop then reveals the rows of nw.  Unrolled over the 16
+        // rows the reveal was 14 KB of the kernel's code (the
+        // instruction cache); the LDS round trip costs 16 ds_write_b128 per unit
+        // and one ds_read_b128 per revealed row.
+        const uint32_t sb = lds0 + (uint32_t)u * (16u * 1024u) + lane() * 16u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            *(lds_u4 *)(uintptr_t)(sb + i * 2048u) = u32x4{V[i][0], V[i][1], V[i][2], V[i][3]};
+            *(lds_u4 *)(uintptr_t)(sb + i * 2048u + 1024u) = u32x4{V[i][4], V[i][5], V[i][6], V[i][7]};
+        }
+        uint32_t rem = nw;
         // (loading the next revealed row's table and output row while this one
         // is multiplied measured no faster: C4 x 16 1648 vs 1657-1666 us, same box)
-        sfor<16>([&](auto T) __attribute__((always_inline)) {
-            constexpr int t = decltype(T)::value;
-            if ((nw >> t) & 1u) {
-                const int r = 16 * u + t;
-                const int j = (r >= a.m ? j_hi : j_lo) + __builtin_popcount(nw & ((1u << t) - 1u));
-                uint32_t o[4];
-                uint32_t y[4] = {bytes(t)[0], bytes(t)[1], bytes(t)[2], bytes(t)[3]};
-                mul16(o, y, tab_at<20>(ctab(a.tw_out) + (uint64_t)j * kTw16));
-                swap32(o[0], o[2]);  // back to lo bytes (p = 0) / hi bytes (p = 1) of symbols 16g..16g+15
-                swap32(o[1], o[3]);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{o[0], o[1], o[2], o[3]}, row_rsrc(a, dst_row(a, j)), off, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        });
+#pragma nounroll
+        while (rem) {
+            const int t = __builtin_ctz(rem);
+            rem &= rem - 1u;
+            const int r = 16 * u + t;
+            const int j = (r >= a.m ? j_hi : j_lo) + __builtin_popcount(nw & ((1u << t) - 1u));
+            const u32x4 x = *(const lds_u4 *)(uintptr_t)(sb + (uint32_t)(t >> 1) * 2048u + (uint32_t)(t & 1) * 1024u);
+            uint32_t o[4];
+            const uint32_t y[4] = {x[0], x[1], x[2], x[3]};
+            mul16(o, y, tab_at<20>(ctab(a.tw_out) + (uint64_t)j * kTw16));
+            swap32(o[0], o[2]);  // back to lo bytes (p = 0) / hi bytes (p = 1) of symbols 16g..16g+15
+            swap32(o[1], o[3]);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{o[0], o[1], o[2], o[3]}, row_rsrc(a, dst_row(a, j)), off, 0, 0);
+        }
     }
 };
 
