@@ -36,10 +36,10 @@ extern "C" {
 #define RS_ERR_TOO_FEW_SHARDS       3  /* ErrTooFewShards       reedsolomon.go:18 */
 #define RS_ERR_SHARD_NO_DATA        4  /* ErrShardNoData        reedsolomon.go:19 */
 #define RS_ERR_SHARD_SIZE           5  /* ErrShardSize          reedsolomon.go:20 */
-#define RS_ERR_INVALID_SHARD_SIZE   6  /* ErrInvalidShardSize   reedsolomon.go:25 */
-#define RS_ERR_NOT_SUPPORTED        7  /* ErrNotSupported       reedsolomon.go:27 */
-#define RS_ERR_SHORT_DATA           8  /* ErrShortData          reedsolomon.go:26 */
-#define RS_ERR_RECONSTRUCT_REQUIRED 9  /* ErrReconstructRequired reedsolomon.go:24 */
+#define RS_ERR_INVALID_SHARD_SIZE   6  /* ErrInvalidShardSize   reedsolomon.go:26 */
+#define RS_ERR_NOT_SUPPORTED        7  /* ErrNotSupported       reedsolomon.go:28 */
+#define RS_ERR_SHORT_DATA           8  /* ErrShortData          reedsolomon.go:27 */
+#define RS_ERR_RECONSTRUCT_REQUIRED 9  /* ErrReconstructRequired reedsolomon.go:25 */
 /* Conditions that have no sentinel in the reference: */
 #define RS_ERR_PANIC               50  /* the Go code panics (slice index out of range) for this geometry */
 #define RS_ERR_NOMEM               51  /* host or device allocation failed */

@@ -19,6 +19,8 @@ from .codec import (  # noqa: F401
     ErrNotSupported,
     ErrShortData,
     ErrReconstructRequired,
+    ErrNilWriter,
+    ErrSize,
     ErrPanic,
     ErrDevice,
     alloc_pinned,
@@ -29,6 +31,6 @@ from ._capi import LIB_PATH, lib  # noqa: F401
 __all__ = [
     "New", "New8", "New16", "ReedSolomon", "RSError", "ErrInvShardNum", "ErrMaxShardNum", "ErrTooFewShards",
     "ErrShardNoData", "ErrShardSize", "ErrInvalidShardSize", "ErrNotSupported", "ErrShortData",
-    "ErrReconstructRequired", "ErrPanic", "ErrDevice", "LIB_PATH", "lib", "alloc_pinned",
+    "ErrReconstructRequired", "ErrNilWriter", "ErrSize", "ErrPanic", "ErrDevice", "LIB_PATH", "lib", "alloc_pinned",
     "EmptyShard",
 ]

@@ -44,10 +44,13 @@ _ERRORS = {
     3: _mk("ErrTooFewShards", 3, "reedsolomon.go:18"),
     4: _mk("ErrShardNoData", 4, "reedsolomon.go:19"),
     5: _mk("ErrShardSize", 5, "reedsolomon.go:20"),
-    6: _mk("ErrInvalidShardSize", 6, "reedsolomon.go:25"),
-    7: _mk("ErrNotSupported", 7, "reedsolomon.go:27"),
-    8: _mk("ErrShortData", 8, "reedsolomon.go:26"),
-    9: _mk("ErrReconstructRequired", 9, "reedsolomon.go:24"),
+    6: _mk("ErrInvalidShardSize", 6, "reedsolomon.go:26"),
+    7: _mk("ErrNotSupported", 7, "reedsolomon.go:28"),
+    8: _mk("ErrShortData", 8, "reedsolomon.go:27"),
+    9: _mk("ErrReconstructRequired", 9, "reedsolomon.go:25"),
+    # host-side only (StreamJoin, stream.py); the C-ABI never returns these
+    10: _mk("ErrNilWriter", 10, "reedsolomon.go:31"),
+    11: _mk("ErrSize", 11, "reedsolomon.go:32"),
     50: _mk("ErrPanic", 50, "the Go reference panics (index out of range) for this geometry"),
     51: _mk("ErrNoMem", 51, "allocation failed"),
     52: _mk("ErrDevice", 52, "HIP device error"),
@@ -62,6 +65,8 @@ ErrInvalidShardSize = _ERRORS[6]
 ErrNotSupported = _ERRORS[7]
 ErrShortData = _ERRORS[8]
 ErrReconstructRequired = _ERRORS[9]
+ErrNilWriter = _ERRORS[10]
+ErrSize = _ERRORS[11]
 ErrPanic = _ERRORS[50]
 ErrDevice = _ERRORS[52]
 
@@ -230,8 +235,12 @@ class ReedSolomon:
         self.device = device
         self._arena = _PinnedArena()
         self._ref_inv = True  # rs_set_reference_inversion_cache default
+        self._streamer = None
 
     def close(self):
+        st, self._streamer = getattr(self, "_streamer", None), None
+        if st is not None and st.rs is not self:
+            st.rs.close()
         if getattr(self, "_h", None):
             self._L.rs_free(self._h)
             self._h = None
@@ -485,6 +494,67 @@ class ReedSolomon:
         out = np.empty(out_size, dtype=np.uint8)
         _check(self._L.rs_join(self._h, ptrs, lens, k, out.ctypes.data if out_size else None, out_size, None))
         return out
+
+    # ---------------- Stream* methods of the ReedSolomon interface
+    # (reedsolomon.go:52-58; rsFF8 :123-228, rsFF16 :231-336)
+    def _stream(self):
+        """The stream codec each Stream* call of the reference builds afresh
+        (newStreamEncoderFF16 / newStreamEncoderFF8).  Kept across calls here
+        (its pinned block buffers are reused).  GF(2^16) streams run on this
+        codec.  GF(2^8) ones get a codec of their own, as in the reference
+        (newFF8, reedsolomon.go:132), whose inversion cache stream.py clears
+        per call, so the caller's cache is left as it was."""
+        if self._streamer is None:
+            from . import stream
+
+            if self.field_bits == 16:
+                self._streamer = stream.StreamEncoder16(self.data_shards(), self.parity_shards(), codec=self)
+            else:
+                own = ReedSolomon(self.data_shards(), self.parity_shards(), 8, self.device)
+                self._streamer = stream.StreamEncoder8(self.data_shards(), self.parity_shards(), codec=own)
+        return self._streamer
+
+    def stream_encode(self, inputs: Sequence, outputs: Sequence) -> None:
+        """StreamEncode (reedsolomon.go:124-138, :232-247)."""
+        if len(inputs) != self.data_shards() or len(outputs) != self.parity_shards():
+            raise ErrTooFewShards("too few shards given")
+        self._stream().encode(inputs, outputs)
+
+    def stream_verify(self, shards: Sequence) -> bool:
+        """StreamVerify (reedsolomon.go:141-154, :250-263)."""
+        if len(shards) != self.total_shards():
+            raise ErrTooFewShards("too few shards given")
+        return self._stream().verify(shards)
+
+    def stream_reconstruct(self, inputs: Sequence, outputs: Sequence) -> None:
+        """StreamReconstruct (reedsolomon.go:156-189, :265-298): the stream's
+        reconstructData when no parity output is requested, else its
+        reconstruct."""
+        st = self._stream()
+        st._check_io(inputs, outputs)
+        if all(outputs[i] is None for i in range(self.data_shards(), self.total_shards())):
+            st.reconstruct_data(inputs, outputs)
+        else:
+            st.reconstruct(inputs, outputs)
+
+    def stream_reconstruct_data(self, inputs: Sequence, outputs: Sequence) -> None:
+        """StreamReconstructData (reedsolomon.go:191-202, :300-310): the data
+        outputs only, through StreamReconstruct."""
+        k = self.data_shards()
+        masked = [outputs[i] if i < k else None for i in range(self.total_shards())]
+        self.stream_reconstruct(inputs, masked)
+
+    def stream_split(self, data, dst: Sequence, size: int) -> None:
+        """StreamSplit (reedsolomon.go:204-215, :312-323)."""
+        from .stream import stream_split
+
+        stream_split(self.data_shards(), data, dst, size)
+
+    def stream_join(self, dst, shards: Sequence, out_size: int) -> None:
+        """StreamJoin (reedsolomon.go:217-228, :325-336)."""
+        from .stream import stream_join
+
+        stream_join(self.data_shards(), self.parity_shards(), dst, shards, out_size)
 
     # ---------------- device-resident operations (torch CUDA tensors)
     def encode_dev(self, rows, stream=None) -> None:

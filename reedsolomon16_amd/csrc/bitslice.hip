@@ -420,12 +420,15 @@ hipError_t launch_hp_t(bool verify, BsArgs a, int cus, hipStream_t s) {
     // take C3 launches of 224-512 full-row stripes from 0.65 to 0.69-0.71 on
     // five of six boxes (one lost 0.01); adjacent tiles or a one- to
     // sixteen-stripe distance lose (0.64-0.667).  Launches under ~200 tiles
-    // per workgroup slot (<= 192 full-row stripes, byte-range slices of 256
-    // stripes) gain little or lose on some boxes, so they keep one tile per
-    // workgroup.
+    // per workgroup slot of full 1 MiB rows (<= 192 stripes) lose 0.01-0.02
+    // with several tiles, so they keep one.  Rows of a byte-range slice
+    // (<= 512 KiB: the per-rank shape of a 2-8 rank split, 256 stripes) never
+    // lost on three boxes with four tiles and gained 0.002-0.06 (profiles/
+    // r05_c3_tiles_per_wg.txt, calls r5h, r5k, r5m).
     const int slots = std::max(cus, 1) * kHpWgPerCu<LOGM>;
     int tpw = hp_tiles_override();
-    if (tpw <= 0) tpw = a.ntiles >= 224 * slots ? 4 : 1;
+    if (tpw <= 0)
+        tpw = (a.ntiles >= 224 * slots || (a.tiles_per_stripe <= 256 && a.ntiles >= 32 * slots)) ? 4 : 1;
     int step = hp_step_override();
     if (step <= 0) step = (a.ntiles + tpw - 1) / tpw;
     step = std::min(step, a.ntiles);

@@ -62,8 +62,8 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from .codec import (EmptyShard, New8, New16, RSError, ErrInvShardNum, ErrPanic, ErrShardNoData,
-                    ErrTooFewShards)
+from .codec import (EmptyShard, New8, New16, RSError, ErrInvShardNum, ErrNilWriter, ErrPanic,
+                    ErrShardNoData, ErrShortData, ErrSize, ErrTooFewShards)
 
 BLOCK_SIZE = 4 * 1024 * 1024  # streaming16.go:48, streaming8.go:83
 
@@ -120,6 +120,174 @@ def _write(writer, buf: np.ndarray, stream: int) -> None:
         raise StreamWriteError(e, stream) from e
     if n is not None and n != len(buf):
         raise StreamWriteError("short write", stream)
+
+
+def _read_once(reader, n: int) -> bytes:
+    """One io.Reader.Read of at most `n` bytes (b"" = io.EOF)."""
+    return bytes(reader.read(n)) if n > 0 else b""
+
+
+def stream_split(data_shards: int, data, dst: Sequence, size: int) -> None:
+    """StreamSplit: rsStream16.split (streaming16.go:635-754) and
+    rsStreamFF8.split (streaming8.go:769-876), which compute the same layout
+    (GF(2^16)'s extra rounding to an even size is absorbed by the 64-byte one).
+
+    Shards 0..k-2 get ``per`` bytes and the last one the remainder, each written
+    zero-padded to a multiple of 64.  ``per`` is ceil64(ceil64(size) / k); when
+    that leaves the last shard nothing, ``per`` becomes ceil64((size - 1) /
+    (k - 1)) and the last shard at least 1 byte.  ``per`` can be 0 (k > 64 with
+    a small size): the first k - 1 writers then receive empty writes and the
+    last shard all the data.  A reader that ends inside the data: the partial
+    shard is written padded, then the next shard's read finds end of stream and
+    the call returns ErrShortData with the earlier shards already written.  A
+    reader that ends after all ``size`` bytes while shards remain fills them
+    with zeros of the current shard's padded length (:720-728).  Reader and
+    writer errors pass through unwrapped, as in the Go code."""
+    if len(dst) != data_shards:
+        raise ErrTooFewShards("too few shards given")
+    if size <= 0:
+        raise ErrShortData("not enough data to fill the number of requested shards")
+    k = data_shards
+    per = _ceil64(_ceil64(size) // k)
+    last = size - per * (k - 1)
+    if last <= 0:  # :668-681
+        per = _ceil64((size - 1) // (k - 1))
+        last = size - per * (k - 1)
+        if last <= 0:
+            last = 1
+    last_al = _ceil64(last)
+    buf = np.zeros(max(per, last_al), dtype=np.uint8)
+    total = 0
+    for s in range(k):
+        to_write, want = (last_al, last) if s == k - 1 else (per, per)
+        n = _read_full(data, buf[:want])
+        if n == 0 and want > 0:  # io.ReadFull's io.EOF: nothing read
+            if total < size:
+                raise ErrShortData("not enough data to fill the number of requested shards")
+            zeros = np.zeros(to_write, dtype=np.uint8)
+            for i in range(s, k):
+                dst[i].write(memoryview(zeros))
+            return
+        total += n
+        out = np.zeros(to_write, dtype=np.uint8)
+        out[:n] = buf[:n]
+        dst[s].write(memoryview(out))
+
+
+def stream_join(data_shards: int, parity_shards: int, dst, shards: Sequence, out_size: int) -> None:
+    """StreamJoin: rsStream16.join (streaming16.go:882-1196) and rsStreamFF8.join
+    (streaming8.go:1003-1320, the same code): writes `out_size` bytes of the
+    data shards' concatenation to `dst`.  Readers are file-like (``read``;
+    None = nil); every branch of the Go code is kept, since each reads the
+    shards differently:
+
+    * ``out_size <= k``: io.ReadFull from each non-nil reader in turn (parity
+      readers included) until ``out_size`` bytes are in;
+    * given k + p readers, only the first k are used; fewer than k non-nil
+      ones is ErrTooFewShards;
+    * ``out_size < 1000``: ONE Read per non-nil shard of the bytes still
+      missing (a short read is not retried: ErrShortData);
+    * every reader seekable (``seek``, the io.Seeker assertion) and
+      ``out_size <= 10 MiB``: each shard read up to ``per`` = ceil64(ceil(out_size
+      / k)) bytes, the last slot up to what is still missing, copied through
+      (joinWithMultiReader :1022-1072; bytes are written before a short result
+      is reported);
+    * otherwise per-shard reads of up to ``per`` bytes in 64 KiB pieces, the
+      last slot's reader (or, when that slot is nil, the last non-nil one)
+      read on to end of stream (joinWithBufferedReads :1074-1196)."""
+    if dst is None:
+        raise ErrNilWriter("the destination writer must not be nil")
+    if len(shards) == 0:
+        raise ErrTooFewShards("too few shards given")
+    if out_size <= 0:
+        raise ErrSize("invalid size")
+    k = data_shards
+    if out_size <= k:  # :896-923
+        got = bytearray()
+        for rd in shards:
+            if rd is None:
+                continue
+            view = np.zeros(out_size - len(got), dtype=np.uint8)
+            n = _read_full(rd, view)
+            got += view[:n].tobytes()
+            if len(got) >= out_size:
+                break
+        if len(got) < out_size:
+            raise ErrShortData("not enough data to fill the number of requested shards")
+        dst.write(bytes(got))
+        return
+    if len(shards) == data_shards + parity_shards:  # :927-929
+        shards = shards[:k]
+    if sum(rd is not None for rd in shards) < k:  # :932-941
+        raise ErrTooFewShards("too few shards given")
+    if out_size < 1000:  # :976-1010
+        got = bytearray()
+        for rd in shards:
+            if rd is None:
+                continue
+            left = out_size - len(got)
+            if left <= 0:
+                break
+            got += _read_once(rd, left)
+            if len(got) >= out_size:
+                break
+        if len(got) < out_size:
+            raise ErrShortData("not enough data to fill the number of requested shards")
+        dst.write(bytes(got[:out_size]))
+        return
+    per = _ceil64(-(-out_size // k))
+    if out_size <= 10 * 1024 * 1024 and all(rd is None or hasattr(rd, "seek") for rd in shards):
+        limits = []
+        for i, rd in enumerate(shards):  # :1036-1057
+            if rd is None:
+                continue
+            want = per
+            if i == len(shards) - 1:
+                want = out_size - len(limits) * per
+                if want <= 0:
+                    break
+            limits.append((rd, want))
+        written = 0
+        for rd, want in limits:
+            view = np.zeros(min(want, out_size - written), dtype=np.uint8)
+            n = _read_full(rd, view)
+            if n:
+                dst.write(view[:n].tobytes())
+            written += n
+            if written >= out_size:
+                break
+        if written < out_size:
+            raise ErrShortData("not enough data to fill the number of requested shards")
+        return
+    piece = 64 * 1024
+    written = 0
+    last_i, last_rd = -1, None
+    for i, rd in enumerate(shards):  # :1098-1155
+        if rd is None:
+            continue
+        last_i, last_rd = i, rd
+        if i == len(shards) - 1 and written < out_size:
+            continue
+        got = 0
+        while got < per and written < out_size:
+            want = min(piece, per - got, out_size - written)
+            if want == 0:
+                break
+            b = _read_once(rd, want)
+            if not b:
+                break
+            dst.write(b)
+            got += len(b)
+            written += len(b)
+    if last_i >= 0 and written < out_size:  # :1158-1188
+        while written < out_size:
+            b = _read_once(last_rd, min(piece, out_size - written))
+            if not b:
+                break
+            dst.write(b)
+            written += len(b)
+    if written < out_size:
+        raise ErrShortData("not enough data to fill the number of requested shards")
 
 
 class _StreamCodec:
@@ -304,6 +472,15 @@ class _StreamCodec:
         for i in range(self.total):
             if inputs[i] is not None and outputs[i] is not None:
                 raise ErrReconstructMismatch("a shard cannot be both an input and an output")
+
+    # ------------------------------------------------------------------ split / join
+    def split(self, data, dst: Sequence, size: int) -> None:
+        """StreamSplit (reedsolomon.go:204-215, :312-323): see stream_split."""
+        stream_split(self.k, data, dst, size)
+
+    def join(self, dst, shards: Sequence, out_size: int) -> None:
+        """StreamJoin (reedsolomon.go:217-228, :325-336): see stream_join."""
+        stream_join(self.k, self.p, dst, shards, out_size)
 
     def _fresh_codec(self) -> None:
         """Every rsFF8 Stream* call builds its own rsStreamFF8 and newFF8

@@ -1,0 +1,55 @@
+"""The reference's stream test suites (reedsolomon_test.go:521-1496,
+hybrid_test.go, mode_comparison_test.go, alignment_test.go; replayed by
+tests/ref_suites.py) through the MI355X engine: the ReedSolomon interface's
+Stream* methods (New16 / New / New8 codecs, each stream call on the HIP
+kernels) against the restated Go loops answered by the oracle.  Every byte a
+writer receives, every verdict and error must match, and the Go test's own
+assertions must hold."""
+import pytest
+
+import reedsolomon16_amd as rs
+from tests import ref_suites
+
+pytestmark = pytest.mark.gpu
+
+
+def _codec(case, k, p, bits):
+    # the constructor each Go test uses: New16 for FF16, New (GF(2^8) for
+    # k + p <= 256) for FF8, New8 in alignment_test.go:45
+    if bits == 16:
+        return rs.New16(k, p)
+    return rs.New8(k, p) if case.startswith("Alignment") else rs.New(k, p)
+
+
+@pytest.mark.parametrize("case", sorted(ref_suites.CASES))
+def test_gpu_reference_stream_suite_case(case):
+    _, k, p, _, bits = ref_suites.CASES[case]
+    want, want_checks = ref_suites.run(ref_suites.GoRS(k, p, bits, 64 * 1024), case)
+    c = _codec(case, k, p, bits)
+    assert c.field_bits == bits
+    try:
+        got, got_checks = ref_suites.run(c, case)
+    finally:
+        c.close()
+    assert got == want
+    assert got_checks == want_checks
+    assert [d for d, ok in got_checks if not ok] == ref_suites.REFERENCE_FAILS.get(case, [])
+
+
+def test_gpu_stream_methods_reuse_one_stream_codec():
+    """Stream* calls on one codec share its pinned block buffers; a GF(2^8)
+    codec's streams run on a codec of their own (fresh inversion cache per
+    call, reedsolomon.go:132), a GF(2^16) codec's on itself."""
+    c16 = rs.New16(4, 2)
+    c8 = rs.New(4, 2)
+    try:
+        case = "StreamVerify/FF16_Size_32768"
+        ref_suites.run(c16, case)
+        s = c16._stream()
+        ref_suites.run(c16, case)
+        assert c16._stream() is s and s.rs is c16
+        ref_suites.run(c8, "StreamVerify/FF8_Size_32768")
+        assert c8._stream().rs is not c8 and c8._stream().rs.field_bits == 8
+    finally:
+        c16.close()
+        c8.close()
