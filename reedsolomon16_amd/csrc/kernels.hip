@@ -1758,6 +1758,38 @@ hipError_t launch_pass(int bits, bool inverse, uint8_t *work, uint64_t S, int di
     });
 }
 
+// Host-resident pipeline, zero copy: one launch moves every scattered row of a
+// segment over PCIe (the device reads or writes the mapped pinned rows), where
+// hipMemcpy*Async took one copy per run of rows at ~10-15 us each
+// (profiles/r05_host_zero_copy.txt: 54-57 GB/s for 128 rows in and 32 out at
+// any segment width, against 6-20 GB/s for per-row copies).  Block (x, y):
+// 16 KB of columns of entry y.
+template <bool TO_HOST>
+__global__ void __launch_bounds__(256) k_zc_copy(ZcRows r, uint8_t *slab, uint64_t pitch, uint64_t off, uint64_t w) {
+    const int e = blockIdx.y;
+    uint8_t *h = r.host[e] + off;
+    uint8_t *d = slab + (uint64_t)r.slab_row[e] * pitch;
+    const uint64_t c0 = (uint64_t)blockIdx.x * 16384;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t c = c0 + (uint64_t)k * 4096 + (uint64_t)threadIdx.x * 16;
+        if (c < w) {
+            if constexpr (TO_HOST) *(uint4 *)(h + c) = *(const uint4 *)(d + c);
+            else *(uint4 *)(d + c) = *(const uint4 *)(h + c);
+        }
+    }
+}
+
+hipError_t launch_zc_copy(const ZcRows &r, uint8_t *slab, uint64_t pitch, uint64_t off, uint64_t w, bool to_host,
+                          hipStream_t s) {
+    if (r.n <= 0) return hipSuccess;
+    if (r.n > kZcMax || (w & 15)) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((w + 16383) / 16384), (unsigned)r.n);
+    if (to_host) hipLaunchKernelGGL(k_zc_copy<true>, grid, dim3(256), 0, s, r, slab, pitch, off, w);
+    else hipLaunchKernelGGL(k_zc_copy<false>, grid, dim3(256), 0, s, r, slab, pitch, off, w);
+    return hipGetLastError();
+}
+
 hipError_t launch_xor_rows(int bits, uint8_t *dst, const uint8_t *src, uint64_t S, int rows, hipStream_t s) {
     (void)bits;
     return for_y(rows, [&](int y0, int ny) {

@@ -82,6 +82,19 @@ hipError_t launch_gather(int bits, uint8_t *work, uint64_t S, RowSet src, int ro
 hipError_t launch_pass(int bits, bool inverse, uint8_t *work, uint64_t S, int dist, int radix, int groups_active,
                        const uint32_t *tw_pass, hipStream_t s);
 // dst[r] ^= src[r] for r in [0, rows)
+// Zero-copy row moves between a device staging slab and pinned host rows the
+// device maps (codec.cpp host_pipeline): entry i is host row host[i] (device
+// view) <-> slab row slab_row[i].  Passed by value (kernel arguments).
+constexpr int kZcMax = 256;
+struct ZcRows {
+    uint8_t *host[kZcMax];
+    uint16_t slab_row[kZcMax];
+    int n;
+};
+// bytes [off, off + w) of every host row <-> the same bytes' slab row at
+// slab + slab_row * pitch (column 0 = off); w a multiple of 16
+hipError_t launch_zc_copy(const ZcRows &r, uint8_t *slab, uint64_t pitch, uint64_t off, uint64_t w, bool to_host,
+                          hipStream_t s);
 hipError_t launch_xor_rows(int bits, uint8_t *dst, const uint8_t *src, uint64_t S, int rows, hipStream_t s);
 // out.row(r) = work[r]  (verify: compare, set *mismatch)
 hipError_t launch_copy_out(int bits, RowSet out, const uint8_t *work, uint64_t S, int rows, int *mismatch,

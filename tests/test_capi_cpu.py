@@ -150,7 +150,7 @@ def test_debug_set_path_knobs(paths):
     assert rs.New16(128, 32).encode_path == "split16-m32"
     paths("bs", 1)
     assert rs.New16(128, 32).encode_path == "bs16-m32"
-    for knob, value in (("sub", 0), ("prune", 0), ("unit_width", 1), ("unit_width", 0), ("unit_width", -1)):
+    for knob, value in (("sub", 0), ("prune", 0), ("unit_width", 1), ("unit_width", 0), ("unit_width", -1), ("zc", 0)):
         paths(knob, value)
     with pytest.raises(ValueError):
         paths("unit_width", 2)

@@ -518,6 +518,50 @@ def test_host_reconstruct_into_capacity():
     assert np.array_equal(work[er[0]], full[er[0]]) and not np.any(small)
 
 
+# Host reconstruct over pinned rows moves them with zero-copy kernels (one per
+# segment and direction, the device reading / writing the mapped rows,
+# codec.cpp zc_rows); rs_debug_set_path("zc", mask) picks the directions (bit 0 in,
+# bit 1 out; 0 keeps the per-run copies).
+# Both paths against the oracle: rows from one slab and from separate pinned
+# allocations, a shard size of several segments with a ragged last one, both
+# fields, and a pageable input row (no zero copy for that call).
+@pytest.mark.parametrize("zc", [3, 1, 2, 0])
+@pytest.mark.parametrize("bits,k,p,S", [(16, 128, 32, 3 * (1 << 18) + 192), (16, 100, 28, 1 << 16), (8, 10, 4, 1 << 17)])
+@pytest.mark.parametrize("rows", ["slab", "separate", "one_pageable"])
+def test_host_reconstruct_zero_copy(paths, zc, bits, k, p, S, rows):
+    from reedsolomon16_amd import codec as rc
+
+    paths("zc", zc)
+    c = rs.ReedSolomon(k, p, bits)
+    c.set_host_segment(1 << 16)  # several segments per call
+    rng = np.random.default_rng(k + S + zc)
+    data = rand_data(rng, k, S)
+    if rows == "slab":
+        shards = c.alloc_aligned(S, pinned=True)
+    else:
+        shards = [rc.alloc_pinned(S) for _ in range(k + p)]
+        if rows == "one_pageable":
+            shards[3] = np.empty(S, np.uint8)
+    for i in range(k):
+        shards[i][:] = data[i]
+    c.encode(shards)
+    full = [np.array(s, copy=True) for s in shards]
+    er = sorted(rng.choice(k + p, p, replace=False).tolist())
+    if rows == "one_pageable" and 3 in er:
+        er = [i for i in er if i != 3] + [min(set(range(k + p)) - set(er) - {3})]
+    work = list(shards)
+    for i in er:
+        work[i][:] = 0xA5
+        work[i] = rs.EmptyShard(work[i])
+    c.reconstruct(work)
+    ref = orc.Oracle(bits, k, p)
+    e, out = ref.reconstruct([None if i in er else full[i] for i in range(k + p)], True)
+    assert e == 0
+    for i in er:
+        assert np.array_equal(work[i], full[i]), i
+        assert np.array_equal(out[i], full[i]), i
+
+
 # Batched device reconstruct (rs_reconstruct_dev_batch): one erasure pattern
 # over many stripes in one launch, rows at a padded stride and stripes at a
 # padded stripe stride; n <= 256 codecs run the LDS kernel with grid.y =
