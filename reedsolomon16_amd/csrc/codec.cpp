@@ -2090,7 +2090,8 @@ void rs_host_free(void *p) {
 
 int rs_host_register(void *p, size_t bytes) {
     if (!p || bytes == 0) return RS_ERR_INVALID_ARG;
-    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterPortable));
+    // mapped: the host reconstruct's zero-copy kernels address the rows through the device's view (zc_rows)
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterPortable | hipHostRegisterMapped));
     return RS_OK;
 }
 
