@@ -527,7 +527,7 @@ def test_host_reconstruct_into_capacity():
 # fields, and a pageable input row (no zero copy for that call).
 @pytest.mark.parametrize("zc", [3, 1, 2, 0])
 @pytest.mark.parametrize("bits,k,p,S", [(16, 128, 32, 3 * (1 << 18) + 192), (16, 100, 28, 1 << 16), (8, 10, 4, 1 << 17)])
-@pytest.mark.parametrize("rows", ["slab", "separate", "one_pageable"])
+@pytest.mark.parametrize("rows", ["slab", "separate", "one_pageable", "registered"])
 def test_host_reconstruct_zero_copy(paths, zc, bits, k, p, S, rows):
     from reedsolomon16_amd import codec as rc
 
@@ -536,8 +536,16 @@ def test_host_reconstruct_zero_copy(paths, zc, bits, k, p, S, rows):
     c.set_host_segment(1 << 16)  # several segments per call
     rng = np.random.default_rng(k + S + zc)
     data = rand_data(rng, k, S)
+    reg = None
     if rows == "slab":
         shards = c.alloc_aligned(S, pinned=True)
+    elif rows == "registered":
+        # an ordinary host slab pinned in place (rs_host_register: Go's slab held by runtime.Pinner)
+        raw = np.zeros((k + p) * S + 4096, np.uint8)
+        o = (-raw.ctypes.data) % 4096
+        reg = raw[o:o + (k + p) * S]
+        assert c._L.rs_host_register(reg.ctypes.data, reg.nbytes) == 0
+        shards = [reg[i * S:(i + 1) * S] for i in range(k + p)]
     else:
         shards = [rc.alloc_pinned(S) for _ in range(k + p)]
         if rows == "one_pageable":
@@ -560,6 +568,8 @@ def test_host_reconstruct_zero_copy(paths, zc, bits, k, p, S, rows):
     for i in er:
         assert np.array_equal(work[i], full[i]), i
         assert np.array_equal(out[i], full[i]), i
+    if reg is not None:
+        assert c._L.rs_host_unregister(reg.ctypes.data) == 0
 
 
 # Batched device reconstruct (rs_reconstruct_dev_batch): one erasure pattern
