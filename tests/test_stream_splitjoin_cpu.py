@@ -177,3 +177,32 @@ def test_stream_join_above_10_mib_takes_the_buffered_branch():
     shards = _split(2, data)
     assert [len(s) for s in shards] == [5 * 1024 * 1024 + 64, 5 * 1024 * 1024]  # per = ceil64(5 MiB + 32)
     assert _join(2, 1, [io.BytesIO(s) for s in shards], n) == data
+
+
+def _hypothesis():
+    try:
+        import hypothesis  # noqa: F401
+        return True
+    except ImportError:
+        return False
+
+
+@pytest.mark.skipif(not _hypothesis(), reason="hypothesis not installed")
+def test_stream_split_join_properties():
+    """Random (k, size): StreamJoin(StreamSplit(x)) == x through every join
+    branch, every shard a multiple of 64 bytes, at most one shard's worth of
+    zero padding past the data in the non-empty shards."""
+    from hypothesis import given, settings, strategies as st
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.integers(1, 300), st.integers(1, 40000), st.booleans())
+    def check(k, n, seekable):
+        data = bytes((i * 7 + k) % 256 for i in range(n))
+        shards = _split(k, data)
+        assert len(shards) == k
+        assert all(len(s) % 64 == 0 for s in shards)
+        assert sum(len(s) for s in shards) >= n
+        rd = [io.BytesIO(s) if seekable else Chunky(s, 1 << 16) for s in shards]
+        assert _join(k, 3, rd, n) == data
+
+    check()
