@@ -182,6 +182,19 @@ def other_workloads(torch, rs, dev, stream) -> dict:
     out["C5_encode"] = {"config": "1024+256 x 256 KiB, 32 stripes per launch", "kernel_path": c5.encode_path,
                         "kernel_ms": round(ms, 5), "us_per_stripe": round(ms * 1e3 / ns, 2),
                         "alg_bytes_per_launch": alg, "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    # C5 is the north star's 8-GPU byte-range config: one rank's launch holds
+    # its 32 KiB slice of every row (dist.byte_range), 32 stripes
+    from reedsolomon16_amd import dist as rsd
+
+    lo, hi = rsd.byte_range(S, 0, 8)
+    sl = torch.randint(0, 256, (ns, k + p, hi - lo), dtype=torch.uint8, device=dev, generator=g)
+    ms = kernel_ms(lambda: c5.encode_dev_batch(sl, stream), 20)
+    alg = ns * (k + p) * (hi - lo)
+    out["C5_encode_rank_of_8"] = {"config": f"1024+256 x 256 KiB split over 8 ranks: rank 0's {hi - lo} bytes of every row, "
+                                            f"{ns} stripes per launch", "kernel_ms": round(ms, 5),
+                                  "us_per_stripe": round(ms * 1e3 / ns, 2), "alg_bytes_per_launch": alg,
+                                  "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    del sl
     # the C5 repair: 256 erased shards (n = 2048 work rows), 8 stripes of the slab
     ns = 8
     c5.encode_dev_batch(slab[:ns], stream)
