@@ -137,6 +137,19 @@ def load_traffic(kernel_name: str, workload: str, stripes: int, row_bytes: int, 
     return e.get("hbm_bytes_per_launch") if e else None
 
 
+def device_info(torch, dev) -> dict:
+    """What the runtime reports about the GPU the line was measured on (C3's
+    rate differs by up to 0.08 of the roofline between boxes with the same
+    code)."""
+    p = torch.cuda.get_device_properties(dev)
+    out = {"name": p.name, "cus": p.multi_processor_count, "hbm_bytes": p.total_memory}
+    for a in ("gcnArchName", "L2_cache_size", "pci_bus_id", "uuid"):
+        v = getattr(p, a, None)
+        if v is not None:
+            out[a] = str(v) if a == "uuid" else v
+    return out
+
+
 def other_workloads(torch, rs, dev, stream) -> dict:
     """Kernel time of the other BASELINE configs on this GPU, beside the
     headline (reported, not the metric): C4 = reconstruct of 128+32 x 1 MiB
@@ -598,6 +611,7 @@ def main():
             "per_rank_kernel_ms": [round(x, 5) for x in per_rank],
             "world_size": dist.get_world_size() if world > 1 else 1,
             "backend": dist.get_backend() if world > 1 else None,
+            "device": device_info(torch, dev),
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
