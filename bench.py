@@ -150,6 +150,30 @@ def device_info(torch, dev) -> dict:
     return out
 
 
+def copy_rate(torch, dev, stream) -> float:
+    """This box's torch device-to-device copy rate (GB/s of bytes read +
+    written, 2 GiB tensor copies on the launch stream): a reference for
+    comparing C3 lines from different boxes.  torch's copy
+    kernel does not reach the HBM peak, so this is not a ceiling."""
+    n = 1 << 31
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    b = torch.empty(n, dtype=torch.uint8, device=dev)
+    a.fill_(1)
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            b.copy_(a)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(10):
+            b.copy_(a)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * n / (ms * 1e-3) / 1e9
+
+
 def other_workloads(torch, rs, dev, stream) -> dict:
     """Kernel time of the other BASELINE configs on this GPU, beside the
     headline (reported, not the metric): C4 = reconstruct of 128+32 x 1 MiB
@@ -557,10 +581,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el, kern_ms, one_ms, flat_ms = float(t[0]), float(t[1]), float(t[2]) or None, float(t[3]) or None
 
-    other = host = None
+    other = host = calib = None
     if world == 1 and not args.no_other:
         del buf, slab, flat
         torch.cuda.empty_cache()
+        calib = copy_rate(torch, dev, stream)
         other = other_workloads(torch, rs, dev, stream)
         other["C2_encode"] = c2_encode(torch, rs, dev, stream)
         torch.cuda.empty_cache()
@@ -612,6 +637,10 @@ def main():
             "world_size": dist.get_world_size() if world > 1 else 1,
             "backend": dist.get_backend() if world > 1 else None,
             "device": device_info(torch, dev),
+            "calibration": None if calib is None else {
+                "torch_copy_gb_s": round(calib, 1),
+                "note": "2 GiB tensor copy_ on the launch stream, bytes read + written: a box-speed reference "
+                        "for comparing lines from different boxes, not a ceiling (the engine's kernels beat it)"},
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
