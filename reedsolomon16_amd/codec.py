@@ -261,6 +261,12 @@ class ReedSolomon:
     def total_shards(self) -> int:
         return self._L.rs_total_shards(self._h)
 
+    def with_concurrency(self, n: int) -> "ReedSolomon":
+        """WithConcurrency (reedsolomon.go:415-427): the reference's rsFF8 and
+        rsFF16 return themselves unchanged; so does the engine (its concurrency
+        is the GPU's)."""
+        return self
+
     def shard_size_multiple(self) -> int:
         return self._L.rs_shard_size_multiple(self._h)
 

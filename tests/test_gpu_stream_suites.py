@@ -53,3 +53,12 @@ def test_gpu_stream_methods_reuse_one_stream_codec():
     finally:
         c16.close()
         c8.close()
+
+
+def test_gpu_with_concurrency_returns_the_codec():
+    """WithConcurrency (reedsolomon.go:415-427) is a no-op returning the codec."""
+    c = rs.New16(4, 2)
+    try:
+        assert c.with_concurrency(8) is c and c.with_concurrency(0) is c
+    finally:
+        c.close()
