@@ -288,7 +288,10 @@ class _ArrayReader:
         n = min(len(b), len(self.a) - self.off)
         if n <= 0:
             return 0
-        b[:n] = memoryview(self.a)[self.off:self.off + n]
+        import numpy as np
+
+        # a numpy copy, which drops the GIL like a file's readinto does
+        np.copyto(np.frombuffer(b, np.uint8, n), self.a[self.off:self.off + n])
         self.off += n
         return n
 
@@ -300,8 +303,10 @@ class _ArrayWriter:
         self.a, self.off = a, 0
 
     def write(self, b):
+        import numpy as np
+
         n = len(b)
-        self.a[self.off:self.off + n] = b
+        np.copyto(self.a[self.off:self.off + n], np.frombuffer(b, np.uint8, n))
         self.off += n
         return n
 
@@ -375,9 +380,20 @@ def host_resident(rs, blocks: int = 2, block: int = 4 << 20) -> dict:
         assert all(np.array_equal(rebuilt[b, j], src[b * block:(b + 1) * block]) for b in range(blocks))
     out["tickets"] = tick
 
-    # ---- the rsStream16 mirror over readers / writers
-    st = StreamEncoder16(K, P, block_size=block)
+    # ---- the rsStream16 mirror over readers / writers: the reference's
+    # sequential loops, and the same loops with a block's readers and writers
+    # on 8 threads (StreamEncoder16(threads=8); same bytes, stream.py)
     sink = np.empty((P, L), np.uint8)
+    rsink = np.empty((len(erased), L), np.uint8)
+    for threads in (1, 8):
+        out["stream" if threads == 1 else f"stream_threads{threads}"] = _stream_rates(
+            StreamEncoder16(K, P, block_size=block, codec=codec, threads=threads), data, par, sink, rsink, erased, K, P,
+            rate)
+    assert np.array_equal(sink, par)
+    return out
+
+
+def _stream_rates(st, data, par, sink, rsink, erased, K, P, rate) -> dict:
     stream_rates = {}
 
     def s_enc():
@@ -385,8 +401,6 @@ def host_resident(rs, blocks: int = 2, block: int = 4 << 20) -> dict:
 
     def s_ver():
         assert st.verify([_ArrayReader(data[i]) for i in range(K)] + [_ArrayReader(par[j]) for j in range(P)])
-
-    rsink = np.empty((len(erased), L), np.uint8)
 
     def s_rec():
         ins = [None if i in erased else _ArrayReader(data[i] if i < K else par[i - K]) for i in range(K + P)]
@@ -401,9 +415,7 @@ def host_resident(rs, blocks: int = 2, block: int = 4 << 20) -> dict:
         t0 = time.perf_counter()
         fn()
         stream_rates[name] = rate(name, time.perf_counter() - t0, rd, wr)
-    assert np.array_equal(sink, par)
-    out["stream"] = stream_rates
-    return out
+    return stream_rates
 
 
 def free_port() -> int:

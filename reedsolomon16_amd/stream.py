@@ -298,7 +298,7 @@ class _StreamCodec:
     EVEN = True  # GF(2^16) pads an odd block to even first (streaming16.go:122-125, :274-287)
 
     def __init__(self, data_shards: int, parity_shards: int, device: Optional[int] = None,
-                 block_size: int = BLOCK_SIZE, depth: int = 2, codec=None):
+                 block_size: int = BLOCK_SIZE, depth: int = 2, codec=None, threads: int = 1):
         if data_shards <= 0 or parity_shards <= 0:  # streaming16.go:36-41, streaming8.go:71-76
             raise ErrInvShardNum("invalid number of shards")
         if self.EVEN and block_size % 2:  # streaming16.go:54-56
@@ -317,6 +317,32 @@ class _StreamCodec:
         self.block_size = block_size
         self.depth = depth
         self._bufs = None
+        # threads > 1: a block's readers are read, and its writers written,
+        # on a pool of that many threads (file readers release the GIL in
+        # readinto).  The bytes every reader and writer sees are the same as
+        # the reference's sequential loops; what differs is only that a
+        # failing reader no longer stops the reads of the readers after it
+        # (the error reported is still the lowest-index one).
+        self._pool = None
+        if threads > 1:
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._pool = ThreadPoolExecutor(max_workers=threads)
+
+    def _each(self, jobs) -> None:
+        """Run every job; re-raise the lowest-index job's exception."""
+        if self._pool is None or len(jobs) < 2:
+            for j in jobs:
+                j()
+            return
+        from concurrent.futures import wait
+
+        futs = [self._pool.submit(j) for j in jobs]
+        wait(futs)  # every job is done with the block buffers before anything is raised
+        for f in futs:
+            e = f.exception()
+            if e is not None:
+                raise e
 
     def _buffers(self):
         # AllocAligned(totalShards, blockSize) (streaming16.go:66-76,
@@ -330,19 +356,19 @@ class _StreamCodec:
         """The read loop every stream operation opens with: io.ReadFull of up
         to blockSize bytes per non-nil reader into its row; returns the first
         non-empty read's length (-1 if none), appends every row's length."""
-        size = -1
-        for i, rd in enumerate(readers):
-            if rd is None:
-                lens.append(0)
-                continue
-            try:
-                n = _read_full(rd, rows[i][:self.block_size])
-            except Exception as e:
-                raise StreamReadError(e, i) from e
-            if n > 0 and size == -1:
-                size = n
-            lens.append(n)
-        return size
+        got = [0] * len(readers)
+
+        def job(i, rd):
+            def run():
+                try:
+                    got[i] = _read_full(rd, rows[i][:self.block_size])
+                except Exception as e:
+                    raise StreamReadError(e, i) from e
+            return run
+
+        self._each([job(i, rd) for i, rd in enumerate(readers) if rd is not None])
+        lens.extend(got)
+        return next((n for n in got if n > 0), -1)
 
     # ------------------------------------------------------------------ encode
     def _read_inputs(self, readers, rows) -> int:
@@ -374,9 +400,8 @@ class _StreamCodec:
             t, rows, size = pending.popleft()
             t.wait()
             al = _ceil64(size)  # writeOutputs (streaming16.go:173-197, streaming8.go:318-340)
-            for j, w in enumerate(outputs):
-                if w is not None:
-                    _write(w, rows[self.k + j][:al], self.k + j)
+            self._each([(lambda w=w, j=j: _write(w, rows[self.k + j][:al], self.k + j))
+                        for j, w in enumerate(outputs) if w is not None])
 
         blk = 0
         try:
@@ -506,6 +531,7 @@ class _StreamCodec:
         def drain_one():
             t, blk_shards, size, al = pending.popleft()
             t.wait()
+            jobs = []
             for i, w in enumerate(outputs):
                 if w is None or not missing[i]:
                     continue
@@ -515,7 +541,8 @@ class _StreamCodec:
                     ws = size  # streaming16.go:618-630, streaming8.go:752-764
                 else:
                     ws = size if i < self.k else al  # streaming16.go:445-464
-                _write(w, np.asarray(blk_shards[i])[:ws], i)
+                jobs.append(lambda w=w, i=i, ws=ws: _write(w, np.asarray(blk_shards[i])[:ws], i))
+            self._each(jobs)
 
         blk, read = 0, 0
         try:
@@ -615,7 +642,6 @@ class StreamEncoder8(_StreamCodec):
             t = self.rs.reconstruct_async([r[:al] for r in rows], recover_all)  # all present: a no-op
             t.wait()
             read += size
-            for i, w in enumerate(outputs):
-                if w is not None:
-                    _write(w, rows[i][:size if i < self.k else al], i)
+            self._each([(lambda w=w, i=i: _write(w, rows[i][:size if i < self.k else al], i))
+                        for i, w in enumerate(outputs) if w is not None])
             blk += 1

@@ -12,7 +12,7 @@ import pytest
 
 from oracle.orc import Oracle
 from reedsolomon16_amd.codec import ErrPanic
-from reedsolomon16_amd.stream import StreamEncoder8, StreamEncoder16
+from reedsolomon16_amd.stream import StreamEncoder8, StreamEncoder16, StreamReadError
 from tests.go_stream import GoPanic, GoStream8, GoStream16
 
 
@@ -461,3 +461,59 @@ def test_stream8_reconstruct_writes_zeros_like_the_reference(n):
         assert m_out[i].getvalue() == go_out[i].getvalue()
     assert go_out[1].getvalue() == bytes(n)
     assert go_out[6].getvalue() == bytes((n + 63) // 64 * 64)
+
+
+def _mirror_threads(k, p, bits, threads, depth=2):
+    fake = OracleTicketCodec(k, p, bits)
+    cls = StreamEncoder16 if bits == 16 else StreamEncoder8
+    return cls(k, p, block_size=BLOCK, depth=depth, codec=fake, threads=threads), fake
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+@pytest.mark.parametrize("case", sorted(ENC_CASES))
+def test_stream_threads_same_bytes_as_go_loop(case, bits):
+    """threads > 1 (a pool reads a block's readers and writes its writers):
+    the codec sees the same blocks and the writers the same bytes as the
+    reference's sequential loops, for encode, verify and reconstruct."""
+    k, p = 6, 3
+    rng = np.random.default_rng(len(case) * 3 + bits)
+    datas = _data(rng, ENC_CASES[case])
+    go = (GoStream16 if bits == 16 else GoStream8)(k, p, BLOCK)
+    gout = [io.BytesIO() for _ in range(p)]
+    go.encode(_streams(datas), gout)
+    st, fake = _mirror_threads(k, p, bits, 4)
+    mout = [io.BytesIO() for _ in range(p)]
+    st.encode(_streams(datas), mout)
+    assert [o.getvalue() for o in mout] == [o.getvalue() for o in gout]
+    if bits == 16:
+        assert fake.calls == go.calls
+    par = [o.getvalue() for o in gout]
+    full = [d if d is not None else b"" for d in datas] + par
+    assert _outcome(st.verify, _streams(full)) == _outcome(go.verify, _streams(full))
+    # reconstruct two data shards into writers
+    if all(d for d in datas):
+        ins = [None if i in (0, 2) else full[i] for i in range(k + p)]
+        outs_m = [io.BytesIO() if i in (0, 2) else None for i in range(k + p)]
+        outs_g = [io.BytesIO() if i in (0, 2) else None for i in range(k + p)]
+        st.reconstruct_data(_streams(ins), outs_m)
+        go.reconstruct_data(_streams(ins), outs_g)
+        assert [o.getvalue() if o else None for o in outs_m] == [o.getvalue() if o else None for o in outs_g]
+
+
+class _Boom:
+    def __init__(self, data, fail):
+        self.b, self.fail = io.BytesIO(data), fail
+
+    def readinto(self, mv):
+        if self.fail:
+            raise OSError("disk gone")
+        return self.b.readinto(mv)
+
+
+def test_stream_threads_report_the_lowest_failing_reader():
+    k, p = 6, 3
+    st, _ = _mirror_threads(k, p, 16, 4)
+    rd = [_Boom(b"x" * 128, fail=i in (2, 5)) for i in range(k)]
+    with pytest.raises(StreamReadError) as ei:
+        st.encode(rd, [io.BytesIO() for _ in range(p)])
+    assert ei.value.stream == 2
