@@ -1193,6 +1193,7 @@ bool zc_rows(uint8_t *const *shards, const std::vector<int> &rows, ZcRows &z) {
     if (rows.size() > (size_t)kZcMax) return false;
     z.n = 0;
     for (int r : rows) {
+        if ((uintptr_t)shards[r] & 15) return false;  // the kernel moves 16-byte words
         hipPointerAttribute_t at{};
         if (hipPointerGetAttributes(&at, shards[r]) != hipSuccess) {
             (void)hipGetLastError();
