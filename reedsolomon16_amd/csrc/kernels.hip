@@ -1032,22 +1032,37 @@ bool pick_narrow(bool automatic) {
     return o < 0 ? automatic : o == 1;
 }
 
-template <class F>
+// PK (the reconstruct kernels, k_rec_lds): 64-byte GF(2^16) tiles (W = 2)
+// keep a unit's 8 low and 8 high bytes together in one 16-byte LDS word,
+// rows unpadded, so each unit access is one ds_read_b128 / ds_write_b128
+// instead of two 8-byte ones, and the lane groups of the n = 2048 passes fall
+// on distinct banks but for a few stores (scripts/lds_bank_model.py:
+// LDS-array cycles 39.9k -> 22.0k per tile, conflict-free 21.5k;
+// profiles/r05_lds_pack_ab.txt).  Otherwise the halves keep their global
+// (Leopard 64-byte block) order in rows padded by 16 bytes; the encoder keeps
+// that layout (packed, its 64-byte-tile variant spills).
+template <class F, bool PK = false>
 struct LTile {
     static_assert(!F::SYM16 || F::W >= 2, "a GF(2^16) LDS tile must cover whole 64-byte blocks (W >= 2)");
     static constexpr bool W16 = F::SYM16;
     static constexpr int TB = 32 * F::W;                  // bytes of each row owned by a workgroup
-    static constexpr int ROW = TB + 16;  // LDS row stride (16 bytes of padding)
+    static constexpr bool PACK = PK && W16 && F::W == 2;
+    static constexpr int ROW = PACK ? TB : TB + 16;  // LDS row stride
     static constexpr int UB = W16 ? 8 * F::W : 4 * F::W;  // global bytes per unit
     static constexpr int U = TB / UB;                     // units per tile
     typedef typename F::Vec V;
     // LDS byte offset of unit u's low (h = 0) or high (h = 1) half in `row`
     __device__ static uint32_t loff(int row, int u, int h) {
+        if constexpr (PACK) return (uint32_t)(row * ROW + 16 * u + 8 * h);
         return (uint32_t)(row * ROW + F::off(u) + 32 * h);
     }
     __device__ static V get(const uint8_t *lds, int row, int u) {
         V v;
-        if constexpr (W16) {
+        if constexpr (PACK) {
+            uint32_t x[4];
+            ldw_lds<4>(lds + loff(row, u, 0), x);
+            v.l[0] = x[0], v.l[1] = x[1], v.h[0] = x[2], v.h[1] = x[3];
+        } else if constexpr (W16) {
             ldw_lds<F::W>(lds + loff(row, u, 0), v.l);
             ldw_lds<F::W>(lds + loff(row, u, 1), v.h);
         } else {
@@ -1065,7 +1080,11 @@ struct LTile {
                 for (int i = 0; i < F::W; i++) x[i] = w[i];
             *(__attribute__((address_space(3))) T *)(q) = x;
         };
-        if constexpr (W16) {
+        if constexpr (PACK) {
+            typedef typename VecOf<4>::T T4;
+            const T4 x = {v.l[0], v.l[1], v.h[0], v.h[1]};
+            *(__attribute__((address_space(3))) T4 *)(lds + loff(row, u, 0)) = x;
+        } else if constexpr (W16) {
             st(lds + loff(row, u, 0), v.l);
             st(lds + loff(row, u, 1), v.h);
         } else {
@@ -1080,15 +1099,15 @@ struct LTile {
 // a transform may read its rows from HBM (LdsIn replaced by a loader) and the
 // last may write them out (to HBM, or XOR them into the encoder's
 // accumulator), so the tile is not staged through LDS an extra time.
-template <class F>
+template <class F, bool PK = false>
 struct LdsIO {
     uint8_t *lds;
-    __device__ typename F::Vec operator()(int row, int u) const { return LTile<F>::get(lds, row, u); }
-    __device__ void operator()(int row, int u, const typename F::Vec &v) const { LTile<F>::put(lds, row, u, v); }
+    __device__ typename F::Vec operator()(int row, int u) const { return LTile<F, PK>::get(lds, row, u); }
+    __device__ void operator()(int row, int u, const typename F::Vec &v) const { LTile<F, PK>::put(lds, row, u, v); }
 };
 
 template <class T> struct IsLdsIO : std::false_type {};
-template <class F> struct IsLdsIO<LdsIO<F>> : std::true_type {};
+template <class F, bool PK> struct IsLdsIO<LdsIO<F, PK>> : std::true_type {};
 
 template <class Fn, int... Is>
 __device__ __forceinline__ void cfor_impl(Fn &&f, std::integer_sequence<int, Is...>) {
@@ -1170,11 +1189,11 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
 // as zero, and zero rows transform to zero rows): later passes read those rows.
 // OUT_P1: pass P1 - 1 (the last this call runs) writes through `out` too.
 template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed, int P0 = 0, int P1 = 32, int NT = 256,
-          bool OUT_P1 = false>
+          bool OUT_P1 = false, bool PK = false>
 __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
                                               NeedT need, const In &in, const Out &out) {
     constexpr int N = 1 << LOGN, NP4 = LOGN / 2, NP = NP4 + (LOGN & 1);
-    const LdsIO<F> lio{lds};
+    const LdsIO<F, PK> lio{lds};
     cfor<NP>([=](auto PI) {  // by value: a captured reference to `need` kept it on the stack
         constexpr int p = decltype(PI)::value;
         if constexpr (p >= P0 && p < P1) {  // passes outside [P0, P1) are run by the caller (fused)
@@ -1240,14 +1259,14 @@ __device__ __forceinline__ void sub_swap(typename F::Vec &v, const uint32_t *__r
 }
 
 // LDS sink that changes rows into subfield coordinates on their way in.
-template <class F>
+template <class F, bool PK = false>
 struct LdsPsi {
     uint8_t *lds;
     const uint32_t *dmap;
     __device__ void operator()(int row, int u, const typename F::Vec &v0) const {
         typename F::Vec v = v0;
         sub_swap<F>(v, dmap);
-        LTile<F>::put(lds, row, u, v);
+        LTile<F, PK>::put(lds, row, u, v);
     }
 };
 
@@ -1269,7 +1288,7 @@ template <int LOGN> struct BigSub {
 
 template <class F, class FT, int LOGN, bool BSUB = false>
 __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) {
-    typedef LTile<F> L;
+    typedef LTile<F, true> L;  // packed 64-byte tiles (LTile PK)
     typedef typename F::Vec V;
     constexpr int N = 1 << LOGN, U = L::U, NT = rec_lds_threads<LOGN>();
     constexpr int K = (N * U + NT - 1) / NT;  // derivative outputs per thread
@@ -1325,16 +1344,16 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
             F::store(dst + tile, u, v);
         }
     };
-    const LdsIO<FT> lio{lds};
+    const LdsIO<FT, true> lio{lds};
     typedef F16S<F::W> FS;  // (BSUB only)
     if constexpr (BSUB) {
         // full-field passes, the last one writing subfield coordinates, then subfield passes
-        lds_transform<F, true, LOGN, ScaleIn, LdsPsi<F>, NoNeed, 0, BigSub<LOGN>::NI, NT, true>(
-            lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, LdsPsi<F>{lds, a.tw_dmap});
-        lds_transform<FS, true, LOGN, LdsIO<FS>, LdsIO<FS>, NoNeed, BigSub<LOGN>::NI, 32, NT>(
-            lds, a.mtrunc, a.tw_ifft_sub, NoNeed{}, LdsIO<FS>{lds}, LdsIO<FS>{lds});
+        lds_transform<F, true, LOGN, ScaleIn, LdsPsi<F, true>, NoNeed, 0, BigSub<LOGN>::NI, NT, true, true>(
+            lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, LdsPsi<F, true>{lds, a.tw_dmap});
+        lds_transform<FS, true, LOGN, LdsIO<FS, true>, LdsIO<FS, true>, NoNeed, BigSub<LOGN>::NI, 32, NT, false, true>(
+            lds, a.mtrunc, a.tw_ifft_sub, NoNeed{}, LdsIO<FS, true>{lds}, LdsIO<FS, true>{lds});
     } else {
-        lds_transform<FT, true, LOGN, ScaleIn, LdsIO<FT>, NoNeed, 0, 32, NT>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
+        lds_transform<FT, true, LOGN, ScaleIn, LdsIO<FT, true>, NoNeed, 0, 32, NT, false, true>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
     }
     const Reveal rv{a, tile, sbase, need_of()};
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
@@ -1380,21 +1399,21 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
         if (a.prune) {
             if constexpr (BSUB) {
                 // subfield passes up to FEND, the last one writing normal coordinates back, then full-field
-                lds_transform<FS, false, LOGN, LdsIO<FS>, LdsPsi<F>, NeedT, 1, BigSub<LOGN>::FEND, NT, true>(
-                    lds, a.mtrunc, a.tw_fft_sub, need_of(), LdsIO<FS>{lds}, LdsPsi<F>{lds, a.tw_dmap});
-                lds_transform<F, false, LOGN, LdsIO<F>, Reveal, NeedT, BigSub<LOGN>::FEND, 32, NT>(
-                    lds, a.mtrunc, a.tw_fft, need_of(), LdsIO<F>{lds}, rv);
+                lds_transform<FS, false, LOGN, LdsIO<FS, true>, LdsPsi<F, true>, NeedT, 1, BigSub<LOGN>::FEND, NT, true, true>(
+                    lds, a.mtrunc, a.tw_fft_sub, need_of(), LdsIO<FS, true>{lds}, LdsPsi<F, true>{lds, a.tw_dmap});
+                lds_transform<F, false, LOGN, LdsIO<F, true>, Reveal, NeedT, BigSub<LOGN>::FEND, 32, NT, false, true>(
+                    lds, a.mtrunc, a.tw_fft, need_of(), LdsIO<F, true>{lds}, rv);
             } else {
-                lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NeedT, 1, 32, NT>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
+                lds_transform<FT, false, LOGN, LdsIO<FT, true>, Reveal, NeedT, 1, 32, NT, false, true>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
             }
         } else {
             if constexpr (BSUB) {
-                lds_transform<FS, false, LOGN, LdsIO<FS>, LdsPsi<F>, NoNeed, 1, BigSub<LOGN>::FEND, NT, true>(
-                    lds, a.mtrunc, a.tw_fft_sub, NoNeed{}, LdsIO<FS>{lds}, LdsPsi<F>{lds, a.tw_dmap});
-                lds_transform<F, false, LOGN, LdsIO<F>, Reveal, NoNeed, BigSub<LOGN>::FEND, 32, NT>(
-                    lds, a.mtrunc, a.tw_fft, NoNeed{}, LdsIO<F>{lds}, rv);
+                lds_transform<FS, false, LOGN, LdsIO<FS, true>, LdsPsi<F, true>, NoNeed, 1, BigSub<LOGN>::FEND, NT, true, true>(
+                    lds, a.mtrunc, a.tw_fft_sub, NoNeed{}, LdsIO<FS, true>{lds}, LdsPsi<F, true>{lds, a.tw_dmap});
+                lds_transform<F, false, LOGN, LdsIO<F, true>, Reveal, NoNeed, BigSub<LOGN>::FEND, 32, NT, false, true>(
+                    lds, a.mtrunc, a.tw_fft, NoNeed{}, LdsIO<F, true>{lds}, rv);
             } else {
-                lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NoNeed, 1, 32, NT>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
+                lds_transform<FT, false, LOGN, LdsIO<FT, true>, Reveal, NoNeed, 1, 32, NT, false, true>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
             }
         }
         return;
@@ -1423,9 +1442,9 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
         __syncthreads();
     }
     if (a.prune) {
-        lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NeedT, 0, 32, NT>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
+        lds_transform<FT, false, LOGN, LdsIO<FT, true>, Reveal, NeedT, 0, 32, NT, false, true>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
     } else {
-        lds_transform<FT, false, LOGN, LdsIO<FT>, Reveal, NoNeed, 0, 32, NT>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
+        lds_transform<FT, false, LOGN, LdsIO<FT, true>, Reveal, NoNeed, 0, 32, NT, false, true>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
     }
 }
 
