@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--slices", default="1,2,8")
     ap.add_argument("--tiles", default="0,1,2,4,8")
     ap.add_argument("--steps", default="0", help="hp_step values (tile distance; 0 = the grid size)")
+    ap.add_argument("--tails", default="-1", help="hp_tail values (single-tile tail; -1 = automatic)")
     ap.add_argument("--alloc", type=int, default=0, help="stripes to allocate (0: the largest launched)")
     ap.add_argument("--geom", default="128,32")
     ap.add_argument("--iters", type=int, default=20)
@@ -38,11 +39,12 @@ def main():
         buf = torch.randint(0, 256, (bmax * (K + P) * RS,), dtype=torch.uint8, device="cuda")
         for B in (int(x) for x in a.stripes.split(",")):
             slab = buf[: B * (K + P) * RS].as_strided((B, K + P, W), ((K + P) * RS, RS, 1))
-            for t, stp in [(int(x), int(y)) for x in a.tiles.split(",") for y in a.steps.split(",")]:
-                if t == 1 and stp:
+            for t, stp, tl in [(int(x), int(y), int(z)) for x in a.tiles.split(",") for y in a.steps.split(",") for z in a.tails.split(",")]:
+                if t == 1 and (stp or tl > 0):
                     continue
                 _capi.set_path("hp_tiles", t)
                 _capi.set_path("hp_step", stp)
+                _capi.set_path("hp_tail", tl)
                 st = torch.cuda.current_stream()
                 for _ in range(3):
                     codec.encode_dev_batch(slab, st)
@@ -55,7 +57,7 @@ def main():
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.iters
                 alg = B * (K + P) * W
-                print(json.dumps({"geom": f"{K}+{P}", "stripes": B, "ranks": nsl, "row_bytes": W, "tiles": t, "step": stp, "alloc": bmax,
+                print(json.dumps({"geom": f"{K}+{P}", "stripes": B, "ranks": nsl, "row_bytes": W, "tiles": t, "step": stp, "tail": tl, "alloc": bmax,
                                   "ms": round(ms, 5), "frac": round(alg / (ms * 1e-3) / 8e12, 4)}), flush=True)
         del buf
         torch.cuda.empty_cache()
