@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--slices", default="1,2,8")
     ap.add_argument("--tiles", default="0,1,2,4,8")
     ap.add_argument("--steps", default="0", help="hp_step values (tile distance; 0 = the grid size)")
-    ap.add_argument("--tails", default="-1", help="hp_tail values (single-tile tail; -1 = automatic)")
+    ap.add_argument("--tails", default="-1", help="hp_tail values of a lab build (single-tile tail; -1 = the product, no knob)")
     ap.add_argument("--alloc", type=int, default=0, help="stripes to allocate (0: the largest launched)")
     ap.add_argument("--geom", default="128,32")
     ap.add_argument("--iters", type=int, default=20)
@@ -44,7 +44,8 @@ def main():
                     continue
                 _capi.set_path("hp_tiles", t)
                 _capi.set_path("hp_step", stp)
-                _capi.set_path("hp_tail", tl)
+                if tl != -1:  # lab builds with the hp_tail knob only (profiles/r05_c3_tail_sweep.txt)
+                    _capi.set_path("hp_tail", tl)
                 st = torch.cuda.current_stream()
                 for _ in range(3):
                     codec.encode_dev_batch(slab, st)
