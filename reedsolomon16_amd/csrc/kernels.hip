@@ -1035,10 +1035,11 @@ bool pick_narrow(bool automatic) {
 // PK (the reconstruct kernels, k_rec_lds): 64-byte GF(2^16) tiles (W = 2)
 // keep a unit's 8 low and 8 high bytes together in one 16-byte LDS word,
 // rows unpadded, so each unit access is one ds_read_b128 / ds_write_b128
-// instead of two 8-byte ones, and the lane groups of the n = 2048 passes fall
-// on distinct banks but for a few stores (scripts/lds_bank_model.py:
-// LDS-array cycles 39.9k -> 22.0k per tile, conflict-free 21.5k;
-// profiles/r05_lds_pack_ab.txt).  Otherwise the halves keep their global
+// (256 B per LDS clock) instead of a ds_read2_b64 / ds_write2_b64 of the two
+// halves 32 bytes apart (128 B per clock), and the lane groups of the
+// n = 2048 passes fall on distinct banks but for a few stores
+// (scripts/lds_bank_model.py: LDS-array cycles 53.2k -> 22.0k per tile;
+// SQ_LDS_BANK_CONFLICT -95 %, profiles/r05_sq_counters.txt, r05_lds_pack_ab.txt).  Otherwise the halves keep their global
 // (Leopard 64-byte block) order in rows padded by 16 bytes; the encoder keeps
 // that layout (packed, its 64-byte-tile variant spills).
 template <class F, bool PK = false>
