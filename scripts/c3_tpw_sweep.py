@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--tails", default="-1", help="hp_tail values of a lab build (single-tile tail; -1 = the product, no knob)")
     ap.add_argument("--alloc", type=int, default=0, help="stripes to allocate (0: the largest launched)")
     ap.add_argument("--geom", default="128,32")
+    ap.add_argument("--pad", type=int, default=3584, help="bytes between rows beyond the row (0: rows back to back)")
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     import torch
@@ -29,7 +30,7 @@ def main():
     from reedsolomon16_amd import dist as rsd
 
     K, P = (int(x) for x in a.geom.split(","))
-    S, pad = 1 << 20, 3584
+    S, pad = 1 << 20, a.pad
     codec = rs.New16(K, P)
     bmax = a.alloc or max(int(x) for x in a.stripes.split(","))
     for nsl in (int(x) for x in a.slices.split(",")):
@@ -58,7 +59,7 @@ def main():
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.iters
                 alg = B * (K + P) * W
-                print(json.dumps({"geom": f"{K}+{P}", "stripes": B, "ranks": nsl, "row_bytes": W, "tiles": t, "step": stp, "tail": tl, "alloc": bmax,
+                print(json.dumps({"geom": f"{K}+{P}", "stripes": B, "ranks": nsl, "row_bytes": W, "tiles": t, "step": stp, "tail": tl, "pad": pad, "alloc": bmax,
                                   "ms": round(ms, 5), "frac": round(alg / (ms * 1e-3) / 8e12, 4)}), flush=True)
         del buf
         torch.cuda.empty_cache()
