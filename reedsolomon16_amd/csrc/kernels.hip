@@ -261,6 +261,41 @@ struct F16S : F16<W_> {
     }
 };
 
+// v if keep, else zero (per lane: selects, no branch)
+template <class F>
+__device__ __forceinline__ void keep_if(typename F::Vec &v, bool keep) {
+    if constexpr (F::SYM16) {
+#pragma unroll
+        for (int i = 0; i < F::W; i++) v.l[i] = keep ? v.l[i] : 0u, v.h[i] = keep ? v.h[i] : 0u;
+    } else {
+#pragma unroll
+        for (int i = 0; i < F::W; i++) v.b[i] = keep ? v.b[i] : 0u;
+    }
+}
+
+// A row unit's address for the reconstruct's scale-in (live = false: a
+// readable stand-in whose product is dropped), and the unit as loaded.
+struct RowLoc {
+    const uint8_t *p;
+    int u;
+    bool live;
+};
+template <class F>
+struct RawRow {
+    typename F::Vec y;
+    bool live;
+};
+template <class F>
+__device__ __forceinline__ typename F::Vec scale_row(const RawRow<F> &y, const uint32_t *__restrict__ t) {
+    typename F::Vec v = F::zero();
+    F::mul_add(v, y.y, t);
+    keep_if<F>(v, y.live);
+    return v;
+}
+// Row sources with a split load (raw / scale): the first pass issues an item's row loads together.
+template <class T, class = void> struct HasRaw : std::false_type {};
+template <class T> struct HasRaw<T, std::void_t<decltype(&T::locate)>> : std::true_type {};
+
 // ---------------------------------------------------------------- butterflies
 #define RS_TW_LIVE(t) ((t)[F::LOGIDX] != F::MOD)
 template <class F>
@@ -1147,7 +1182,21 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
             const int i = g * 4 * dist + j;
             if (!INV && !rows_needed(need, g * 4 * dist, 4 * dist)) return;
             const uint32_t *t = tw + (uint64_t)g * 3 * F::TWD;
-            V x0 = in(i, u), x1 = in(i + dist, u), x2 = in(i + 2 * dist, u), x3 = in(i + 3 * dist, u);
+            V x0, x1, x2, x3;
+            if constexpr (HasRaw<In>::value) {
+                // the four rows' addresses, then their loads, then their
+                // scale tables: a load waits only for its own kind (with the
+                // steps interleaved per row every row waited out the previous
+                // row's HBM trip: the memory counter retires in order)
+                const RowLoc l0 = in.locate(i, u), l1 = in.locate(i + dist, u), l2 = in.locate(i + 2 * dist, u),
+                             l3 = in.locate(i + 3 * dist, u);
+                __builtin_amdgcn_sched_barrier(0);
+                const auto r0 = in.fetch(l0), r1 = in.fetch(l1), r2 = in.fetch(l2), r3 = in.fetch(l3);
+                __builtin_amdgcn_sched_barrier(0);
+                x0 = in.scale(i, r0), x1 = in.scale(i + dist, r1), x2 = in.scale(i + 2 * dist, r2), x3 = in.scale(i + 3 * dist, r3);
+            } else {
+                x0 = in(i, u), x1 = in(i + dist, u), x2 = in(i + 2 * dist, u), x3 = in(i + 3 * dist, u);
+            }
             if constexpr (INV) ifft4<F, BF>(x0, x1, x2, x3, t);
             else fft4<F, BF>(x0, x1, x2, x3, t);
             out(i, u, x0);
@@ -1303,23 +1352,39 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
     }
     const uint64_t tile = (uint64_t)bx * L::TB;
     uint8_t *const sbase = a.base ? a.base + (uint64_t)blockIdx.y * a.stripe_stride : nullptr;  // this stripe
-    // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0
-    struct ScaleIn {
+    // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0.
+    // Branch-free, so the four rows of a first-pass item issue their loads
+    // together: a missing row (or a unit past the row end) loads from a
+    // readable stand-in, the scale-in table, and its product is dropped.
+    // (With a branch per row each row waited out its own HBM round trip.)
+    // Two forms: rows at a stride from the stripe base (src_idx), or a row table.
+    // locate(r, u): where the row's unit is; fetch: its load; scale: times
+    // errLocs[r].  lds_pass runs each step for an item's four rows before the
+    // next, so each kind of load waits for its own kind only.
+    struct ScaleInStrided {
         const RecArgs &a;
         uint64_t tile;
         uint8_t *sbase;
-        __device__ V operator()(int r, int u) const {
-            V v = F::zero();
-            const uint8_t *src;
-            if (sbase) {
-                const int i = a.src_idx[r];
-                src = i >= 0 ? sbase + (uint64_t)i * a.stride : nullptr;
-            } else {
-                src = a.src[r];
-            }
-            if (src && L::valid(tile, a.S, u)) F::mul_add(v, F::load(src + tile, u), a.tw_in + (uint64_t)r * F::TWD);
-            return v;
+        __device__ RowLoc locate(int r, int u) const {
+            const int i = a.src_idx[r];
+            const bool live = i >= 0 && L::valid(tile, a.S, u);
+            return RowLoc{live ? sbase + (uint64_t)i * a.stride + tile : (const uint8_t *)a.tw_in, live ? u : 0, live};
         }
+        __device__ RawRow<F> fetch(const RowLoc &l) const { return RawRow<F>{F::load(l.p, l.u), l.live}; }
+        __device__ V scale(int r, const RawRow<F> &y) const { return scale_row<F>(y, a.tw_in + (uint64_t)r * F::TWD); }
+        __device__ V operator()(int r, int u) const { return scale(r, fetch(locate(r, u))); }
+    };
+    struct ScaleInTable {
+        const RecArgs &a;
+        uint64_t tile;
+        __device__ RowLoc locate(int r, int u) const {
+            const uint8_t *src = a.src[r];
+            const bool live = src && L::valid(tile, a.S, u);
+            return RowLoc{live ? src + tile : (const uint8_t *)a.tw_in, live ? u : 0, live};
+        }
+        __device__ RawRow<F> fetch(const RowLoc &l) const { return RawRow<F>{F::load(l.p, l.u), l.live}; }
+        __device__ V scale(int r, const RawRow<F> &y) const { return scale_row<F>(y, a.tw_in + (uint64_t)r * F::TWD); }
+        __device__ V operator()(int r, int u) const { return scale(r, fetch(locate(r, u))); }
     };
     // n > 256: the revealed-row mask and the output indices come from HBM
     constexpr bool BIG = LOGN > 8;
@@ -1349,12 +1414,23 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
     typedef F16S<F::W> FS;  // (BSUB only)
     if constexpr (BSUB) {
         // full-field passes, the last one writing subfield coordinates, then subfield passes
-        lds_transform<F, true, LOGN, ScaleIn, LdsPsi<F, true>, NoNeed, 0, BigSub<LOGN>::NI, NT, true, true>(
-            lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, LdsPsi<F, true>{lds, a.tw_dmap});
+        if (sbase)
+            lds_transform<F, true, LOGN, ScaleInStrided, LdsPsi<F, true>, NoNeed, 0, BigSub<LOGN>::NI, NT, true, true>(
+                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInStrided{a, tile, sbase}, LdsPsi<F, true>{lds, a.tw_dmap});
+        else
+            lds_transform<F, true, LOGN, ScaleInTable, LdsPsi<F, true>, NoNeed, 0, BigSub<LOGN>::NI, NT, true, true>(
+                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInTable{a, tile}, LdsPsi<F, true>{lds, a.tw_dmap});
         lds_transform<FS, true, LOGN, LdsIO<FS, true>, LdsIO<FS, true>, NoNeed, BigSub<LOGN>::NI, 32, NT, false, true>(
             lds, a.mtrunc, a.tw_ifft_sub, NoNeed{}, LdsIO<FS, true>{lds}, LdsIO<FS, true>{lds});
     } else {
-        lds_transform<FT, true, LOGN, ScaleIn, LdsIO<FT, true>, NoNeed, 0, 32, NT, false, true>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleIn{a, tile, sbase}, lio);
+        // the first pass (it reads the rows) per row form, then the rest
+        if (sbase)
+            lds_transform<FT, true, LOGN, ScaleInStrided, LdsIO<FT, true>, NoNeed, 0, 1, NT, false, true>(
+                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInStrided{a, tile, sbase}, lio);
+        else
+            lds_transform<FT, true, LOGN, ScaleInTable, LdsIO<FT, true>, NoNeed, 0, 1, NT, false, true>(
+                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInTable{a, tile}, lio);
+        lds_transform<FT, true, LOGN, LdsIO<FT, true>, LdsIO<FT, true>, NoNeed, 1, 32, NT, false, true>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, lio, lio);
     }
     const Reveal rv{a, tile, sbase, need_of()};
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
