@@ -203,6 +203,44 @@ def test_stream_split_join_properties():
         assert all(len(s) % 64 == 0 for s in shards)
         assert sum(len(s) for s in shards) >= n
         rd = [io.BytesIO(s) if seekable else Chunky(s, 1 << 16) for s in shards]
+        if seekable and _split_per(k, n) != _join_per(k, n):
+            # the reference's own split and seekable join disagree on the
+            # shard size here (test_reference_split_join_size_mismatch)
+            return
         assert _join(k, 3, rd, n) == data
 
     check()
+
+
+def _split_per(k, n):
+    """rsStream16.split's shard size (streaming16.go:645-676): floor of the
+    64-aligned size over k, rounded up to 64; recomputed from (size - 1) /
+    (k - 1) when the last shard would get nothing."""
+    aligned = -(-(n + (n & 1)) // 64) * 64
+    per = -(-(aligned // k) // 64) * 64
+    if n - per * (k - 1) <= 0 and k > 1:
+        per = -(-((n - 1) // (k - 1)) // 64) * 64
+    return per
+
+
+def _join_per(k, n):
+    """joinWithMultiReader's shard size (streaming16.go:1022-1031): the
+    ceiling of size over k, rounded up to 64."""
+    per = -(-n // k)
+    return -(-per // 64) * 64 if per % 64 else per
+
+
+def test_reference_split_join_size_mismatch():
+    """k = 70, 4536 bytes: split writes 64-byte shards (4544 // 70 = 64) but
+    the seekable join expects ceil(4536 / 70) -> 128 per shard, so its last
+    shard's limit goes negative, the multi-reader stops one shard short and
+    the join reports short data -- the reference's behaviour, restated; the
+    buffered (non-seekable) branch reads the last shard to the end and
+    round-trips."""
+    k, n = 70, 4536
+    assert (_split_per(k, n), _join_per(k, n)) == (64, 128)
+    data = bytes((i * 7 + k) % 256 for i in range(n))
+    shards = _split(k, data)
+    with pytest.raises(ErrShortData):
+        _join(k, 3, [io.BytesIO(s) for s in shards], n)
+    assert _join(k, 3, [Chunky(s, 1 << 16) for s in shards], n) == data
