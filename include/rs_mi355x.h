@@ -56,6 +56,34 @@ typedef struct rs_codec rs_codec;
 int rs_new(int field_bits, int data_shards, int parity_shards, int device, rs_codec **out);
 void rs_free(rs_codec *codec);
 
+/* ---------------- Multi-device codec (the byte-range split) ----------------
+ * rs_new_multi: one Encoder (reedsolomon.go:90-93) over `ndevices` GPUs.  Every
+ * Leopard operation is column-local (leopard16.go:778-792), so device g owns
+ * bytes [lo_g, hi_g) of EVERY shard (rs_byte_range: 64-byte blocks dealt as
+ * evenly as possible) and works on them with no data exchange.  The host-
+ * memory entry points (rs_encode / rs_verify / rs_reconstruct, their _async
+ * forms, rs_ticket_wait / _query, rs_verify_result, rs_set_host_segment,
+ * rs_split / rs_join) take the same arguments as for a one-device codec and
+ * give the same results: each device's share runs on a host worker thread of
+ * its own, over that device's streams and PCIe link; verify ANDs the devices'
+ * verdicts on the host; a reconstruct's error locators are computed once and
+ * handed to every device (for GF(2^8) with the reference's inversion-cache
+ * keying on the full shard size, so the call sequence semantics of
+ * rs_set_reference_inversion_cache are unchanged).  devices[] may repeat an
+ * ordinal (several parts on one GPU).  ndevices == 1 returns a plain codec.
+ * The device-resident entry points (rs_*_dev*) return RS_ERR_INVALID_ARG on a
+ * multi-device codec (their rows live on one device): use rs_device_part for
+ * device g's own codec, which the multi-device codec owns (never rs_free it). */
+#define RS_MAX_DEVICES 64
+int rs_new_multi(int field_bits, int data_shards, int parity_shards, const int *devices, int ndevices,
+                 rs_codec **out);
+/* Number of devices (parts) of a codec: 1 for rs_new. */
+int rs_device_count(const rs_codec *codec);
+/* Part `index` of a codec (the codec itself for a one-device codec) and its device ordinal. */
+int rs_device_part(rs_codec *codec, int index, rs_codec **part, int *device);
+/* [*lo, *hi) of the shard bytes part `index` of `nparts` owns; RS_ERR_INVALID_SHARD_SIZE if shard_size % 64. */
+int rs_byte_range(size_t shard_size, int index, int nparts, size_t *lo, size_t *hi);
+
 /* Extensions interface (reedsolomon.go:358-375). */
 int rs_field_bits(const rs_codec *codec);
 int rs_data_shards(const rs_codec *codec);
@@ -151,7 +179,14 @@ int rs_join(rs_codec *codec, uint8_t *const *shards, const size_t *lens, int nsh
  * automatic (about 8 MiB copied in per segment). */
 int rs_set_host_segment(rs_codec *codec, size_t bytes);
 
-/* GF(2^8) reconstruct with the reference's inversion cache semantics
+/* WARNING -- default behaviour that returns WRONG DATA for some call
+ * sequences, exactly as the reference does: every GF(2^8) codec of at most 64
+ * shards keeps the reference's inversion cache (below), so a reconstruct whose
+ * erasure pattern shares the reference's cache key with an earlier call's
+ * rebuilds its shards with that call's locators.  rs_set_reference_inversion_cache
+ * (codec, 0) turns it off (always-correct exact keying).
+ *
+ * GF(2^8) reconstruct with the reference's inversion cache semantics
  * (leopard8.go:508-555, codecs of at most 64 shards: :67-71).  The reference
  * looks its cached errLocs up by the raw erasure bitfield, which leaves out
  * parity erasures unless recoverAll, and stores them under the bitfield after

@@ -27,6 +27,10 @@ def lib() -> C.CDLL:
     L.rs_new.argtypes = [i32, i32, i32, i32, P(vp)]
     L.rs_free.argtypes = [vp]
     L.rs_free.restype = None
+    L.rs_new_multi.argtypes = [i32, i32, i32, P(i32), i32, P(vp)]
+    L.rs_device_count.argtypes = [vp]
+    L.rs_device_part.argtypes = [vp, i32, P(vp), P(i32)]
+    L.rs_byte_range.argtypes = [sz, i32, i32, P(sz), P(sz)]
     for fn in ("rs_field_bits", "rs_data_shards", "rs_parity_shards", "rs_total_shards", "rs_shard_size_multiple"):
         getattr(L, fn).argtypes = [vp]
     L.rs_encode.argtypes = [vp, P(vp), P(sz), i32]

@@ -17,9 +17,11 @@ current torch stream.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import io
 import sys
+import threading
 from typing import Optional, Sequence
 
 import numpy as np
@@ -113,15 +115,17 @@ class _PinnedArena:
 
     def __init__(self):
         self._cur, self._off = None, 0
+        self._lock = threading.Lock()  # tickets may be queued from several threads
 
     def take(self, nbytes: int) -> np.ndarray:
         need = (nbytes + 63) // 64 * 64
         if nbytes > self.BLOCK // 4:
             return alloc_pinned(nbytes)
-        if self._cur is None or self._off + need > len(self._cur):
-            self._cur, self._off = alloc_pinned(self.BLOCK), 0
-        row = self._cur[self._off:self._off + nbytes]
-        self._off += need
+        with self._lock:
+            if self._cur is None or self._off + need > len(self._cur):
+                self._cur, self._off = alloc_pinned(self.BLOCK), 0
+            row = self._cur[self._off:self._off + nbytes]
+            self._off += need
         return row
 
 
@@ -218,8 +222,17 @@ def _stream_handle(stream):
 class ReedSolomon:
     """One encoder instance (leopardFF16 / leopardFF8 behind the ReedSolomon interface)."""
 
-    def __init__(self, data_shards: int, parity_shards: int, field_bits: int = 0, device: Optional[int] = None):
+    def __init__(self, data_shards: int, parity_shards: int, field_bits: int = 0, device: Optional[int] = None,
+                 devices: Optional[Sequence[int]] = None):
+        """devices: a list of device ordinals (repeats allowed) makes one
+        multi-device codec (rs_new_multi): the host-memory operations split
+        every shard by 64-byte byte ranges over them (include/rs_mi355x.h)."""
         L = _capi.lib()
+        if devices is not None:
+            devs = [int(d) for d in devices]
+            if not devs:
+                raise ValueError("devices must name at least one device")
+            device = devs[0]
         if device is None:
             device = 0
             # follow torch's current device only when the caller already uses
@@ -229,20 +242,29 @@ class ReedSolomon:
             if torch is not None and torch.cuda.is_available():
                 device = torch.cuda.current_device()
         h = C.c_void_p()
-        _check(L.rs_new(field_bits, data_shards, parity_shards, device, C.byref(h)))
+        if devices is not None:
+            arr = (C.c_int * len(devs))(*devs)
+            _check(L.rs_new_multi(field_bits, data_shards, parity_shards, arr, len(devs), C.byref(h)))
+        else:
+            _check(L.rs_new(field_bits, data_shards, parity_shards, device, C.byref(h)))
         self._h = h
         self._L = L
         self.device = device
+        self.devices = list(devs) if devices is not None else [device]
         self._arena = _PinnedArena()
         self._ref_inv = True  # rs_set_reference_inversion_cache default
         self._streamer = None
+        self._stream_lock = threading.Lock()
 
     def close(self):
         st, self._streamer = getattr(self, "_streamer", None), None
-        if st is not None and st.rs is not self:
-            st.rs.close()
+        if st is not None:
+            st.close()
+            if st.rs is not self:
+                st.rs.close()
         if getattr(self, "_h", None):
-            self._L.rs_free(self._h)
+            if not getattr(self, "_borrowed", False):  # a part() belongs to its multi-device codec
+                self._L.rs_free(self._h)
             self._h = None
 
     def __del__(self):
@@ -273,6 +295,32 @@ class ReedSolomon:
     @property
     def field_bits(self) -> int:
         return self._L.rs_field_bits(self._h)
+
+    @property
+    def device_count(self) -> int:
+        """Devices the codec splits its host-memory calls over (rs_device_count)."""
+        return self._L.rs_device_count(self._h)
+
+    def part(self, index: int) -> "ReedSolomon":
+        """Device `index`'s own codec (rs_device_part): the codec itself on
+        one device.  For device-resident calls on that device's byte range
+        (byte_range) of rows in its HBM.  Owned by this codec: valid while it
+        is open, never freed on its own."""
+        h, dev = C.c_void_p(), C.c_int(0)
+        _check(self._L.rs_device_part(self._h, index, C.byref(h), C.byref(dev)))
+        if h.value == self._h.value:
+            return self
+        q = ReedSolomon.__new__(ReedSolomon)
+        q._h, q._L, q.device, q.devices = h, self._L, dev.value, [dev.value]
+        q._arena, q._ref_inv, q._streamer, q._stream_lock = _PinnedArena(), False, None, threading.Lock()
+        q._borrowed, q._owner = True, self
+        return q
+
+    def byte_range(self, shard_size: int, index: int):
+        """[lo, hi) of the shard bytes device `index` of this codec owns (rs_byte_range)."""
+        lo, hi = C.c_size_t(0), C.c_size_t(0)
+        _check(self._L.rs_byte_range(shard_size, index, self.device_count, C.byref(lo), C.byref(hi)))
+        return lo.value, hi.value
 
     @property
     def encode_path(self) -> str:
@@ -503,45 +551,74 @@ class ReedSolomon:
 
     # ---------------- Stream* methods of the ReedSolomon interface
     # (reedsolomon.go:52-58; rsFF8 :123-228, rsFF16 :231-336)
-    def _stream(self):
-        """The stream codec each Stream* call of the reference builds afresh
-        (newStreamEncoderFF16 / newStreamEncoderFF8).  Kept across calls here
-        (its pinned block buffers are reused).  GF(2^16) streams run on this
-        codec.  GF(2^8) ones get a codec of their own, as in the reference
-        (newFF8, reedsolomon.go:132), whose inversion cache stream.py clears
-        per call, so the caller's cache is left as it was."""
-        if self._streamer is None:
-            from . import stream
+    # pinned block buffers a codec keeps between Stream* calls (depth x
+    # total x 4 MiB: 1.25 GiB at 128 + 32); larger sets are freed per call
+    STREAM_KEEP_BYTES = 2 << 30
 
-            if self.field_bits == 16:
-                self._streamer = stream.StreamEncoder16(self.data_shards(), self.parity_shards(), codec=self)
-            else:
-                own = ReedSolomon(self.data_shards(), self.parity_shards(), 8, self.device)
-                self._streamer = stream.StreamEncoder8(self.data_shards(), self.parity_shards(), codec=own)
-        return self._streamer
+    def _new_streamer(self):
+        """The stream codec each Stream* call of the reference builds
+        (newStreamEncoderFF16 / newStreamEncoderFF8).  GF(2^16) streams run on
+        this codec.  GF(2^8) ones get a codec of their own, as in the
+        reference (newFF8, reedsolomon.go:132), whose inversion cache
+        stream.py clears per call, so the caller's cache is left as it was."""
+        from . import stream
+
+        if self.field_bits == 16:
+            return stream.StreamEncoder16(self.data_shards(), self.parity_shards(), codec=self)
+        own = ReedSolomon(self.data_shards(), self.parity_shards(), 8, self.device,
+                          devices=self.devices if len(self.devices) > 1 else None)
+        return stream.StreamEncoder8(self.data_shards(), self.parity_shards(), codec=own)
+
+    @contextlib.contextmanager
+    def _stream(self):
+        """A stream codec for one Stream* call.  The codec keeps one and reuses
+        its pinned block buffers across calls (up to STREAM_KEEP_BYTES); a call
+        made while another thread's Stream* call holds it gets a fresh one of
+        its own, so concurrent calls never share block buffers (the reference
+        builds a fresh encoder per call, reedsolomon.go:132,240)."""
+        if self._stream_lock.acquire(blocking=False):
+            try:
+                if self._streamer is None:
+                    self._streamer = self._new_streamer()
+                st = self._streamer
+                yield st
+            finally:
+                if st.depth * st.total * st.block_size > self.STREAM_KEEP_BYTES:
+                    st._bufs = None
+                self._stream_lock.release()
+            return
+        st = self._new_streamer()
+        try:
+            yield st
+        finally:
+            st.close()
+            if st.rs is not self:
+                st.rs.close()
 
     def stream_encode(self, inputs: Sequence, outputs: Sequence) -> None:
         """StreamEncode (reedsolomon.go:124-138, :232-247)."""
         if len(inputs) != self.data_shards() or len(outputs) != self.parity_shards():
             raise ErrTooFewShards("too few shards given")
-        self._stream().encode(inputs, outputs)
+        with self._stream() as st:
+            st.encode(inputs, outputs)
 
     def stream_verify(self, shards: Sequence) -> bool:
         """StreamVerify (reedsolomon.go:141-154, :250-263)."""
         if len(shards) != self.total_shards():
             raise ErrTooFewShards("too few shards given")
-        return self._stream().verify(shards)
+        with self._stream() as st:
+            return st.verify(shards)
 
     def stream_reconstruct(self, inputs: Sequence, outputs: Sequence) -> None:
         """StreamReconstruct (reedsolomon.go:156-189, :265-298): the stream's
         reconstructData when no parity output is requested, else its
         reconstruct."""
-        st = self._stream()
-        st._check_io(inputs, outputs)
-        if all(outputs[i] is None for i in range(self.data_shards(), self.total_shards())):
-            st.reconstruct_data(inputs, outputs)
-        else:
-            st.reconstruct(inputs, outputs)
+        with self._stream() as st:
+            st._check_io(inputs, outputs)
+            if all(outputs[i] is None for i in range(self.data_shards(), self.total_shards())):
+                st.reconstruct_data(inputs, outputs)
+            else:
+                st.reconstruct(inputs, outputs)
 
     def stream_reconstruct_data(self, inputs: Sequence, outputs: Sequence) -> None:
         """StreamReconstructData (reedsolomon.go:191-202, :300-310): the data
@@ -654,16 +731,19 @@ class VerifyTicket(EncodeTicket):
         return bool(ok.value)
 
 
-def New(data_shards: int, parity_shards: int, device: Optional[int] = None) -> ReedSolomon:
+def New(data_shards: int, parity_shards: int, device: Optional[int] = None,
+        devices: Optional[Sequence[int]] = None) -> ReedSolomon:
     """New (reedsolomon.go:69-81): GF(2^8) when data+parity <= 256, else GF(2^16)."""
-    return ReedSolomon(data_shards, parity_shards, 0, device)
+    return ReedSolomon(data_shards, parity_shards, 0, device, devices)
 
 
-def New8(data_shards: int, parity_shards: int, device: Optional[int] = None) -> ReedSolomon:
+def New8(data_shards: int, parity_shards: int, device: Optional[int] = None,
+         devices: Optional[Sequence[int]] = None) -> ReedSolomon:
     """New8 (reedsolomon.go:84-87)."""
-    return ReedSolomon(data_shards, parity_shards, 8, device)
+    return ReedSolomon(data_shards, parity_shards, 8, device, devices)
 
 
-def New16(data_shards: int, parity_shards: int, device: Optional[int] = None) -> ReedSolomon:
+def New16(data_shards: int, parity_shards: int, device: Optional[int] = None,
+          devices: Optional[Sequence[int]] = None) -> ReedSolomon:
     """New16 (reedsolomon.go:90-93)."""
-    return ReedSolomon(data_shards, parity_shards, 16, device)
+    return ReedSolomon(data_shards, parity_shards, 16, device, devices)

@@ -25,6 +25,7 @@
 #include "../../include/rs_mi355x.h"
 #include "gf_host.hpp"
 #include "kernels.hpp"
+#include "multi.hpp"
 #include "schedule.hpp"
 
 using namespace rs;
@@ -236,7 +237,13 @@ struct rs_codec {
     uint8_t *bounce = nullptr;
     size_t bounce_n = 0;
 
+    // rs_new_multi: the per-device parts (this codec then owns no device
+    // resources of its own; its caches hold the reconstruct locators)
+    Multi *multi = nullptr;
+
     ~rs_codec() {
+        if (multi) multi_destroy(multi);  // joins the part workers, frees the parts
+        multi = nullptr;
         if (!dev_ready && !stream) return;
         DeviceGuard g(device);
         if (stream) (void)hipStreamSynchronize(stream);
@@ -745,7 +752,7 @@ const std::vector<uint32_t> *ref_inv_errlocs(rs_codec *c, const std::vector<uint
 }
 
 int plan_reconstruct_new(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
-                         const std::vector<uint32_t> *el_ref, RecPlan &pl);
+                         const std::vector<uint32_t> *el_ref, RecPlan &pl, const std::vector<uint32_t> *el_exact);
 
 // Plan-cache key: (erasure pattern, recover_all), plus the errLocs a
 // reference-keyed cache handed out, which can differ between calls with the
@@ -765,7 +772,7 @@ std::vector<uint8_t> plan_key(const std::vector<uint8_t> &present, bool recover_
 // reference-keyed cache answer (ref_inv_errlocs), looked up by the caller
 // exactly once per reconstruct, as leopard8.go:509-554 looks up and stores once.
 int plan_reconstruct_el(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
-                        const std::vector<uint32_t> *el_ref, RecPlan &pl) {
+                        const std::vector<uint32_t> *el_ref, RecPlan &pl, const std::vector<uint32_t> *el_exact = nullptr) {
     std::vector<uint8_t> key = plan_key(present, recover_all, el_ref);
     for (auto it = c->plan_cache.begin(); it != c->plan_cache.end(); ++it) {
         if (it->first == key) {
@@ -774,25 +781,31 @@ int plan_reconstruct_el(rs_codec *c, const std::vector<uint8_t> &present, bool r
             return RS_OK;
         }
     }
-    int e = plan_reconstruct_new(c, present, recover_all, el_ref, pl);
+    int e = plan_reconstruct_new(c, present, recover_all, el_ref, pl, el_exact);
     if (e) return e;
     c->plan_cache.emplace_front(std::move(key), pl);
     if (c->plan_cache.size() > 16) c->plan_cache.pop_back();
     return RS_OK;
 }
-int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, uint64_t S, RecPlan &pl) {
+// el_ext: locators handed in by a multi-device parent (computed once for all
+// its parts) instead of this codec's own caches.
+int plan_reconstruct(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, uint64_t S, RecPlan &pl,
+                     const ElExt *el_ext = nullptr) {
+    if (el_ext)
+        return plan_reconstruct_el(c, present, recover_all, el_ext->ref ? el_ext->el : nullptr, pl,
+                                   el_ext->ref ? nullptr : el_ext->el);
     return plan_reconstruct_el(c, present, recover_all, ref_inv_errlocs(c, present, recover_all, S), pl);
 }
 
 int plan_reconstruct_new(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
-                         const std::vector<uint32_t> *el_ref, RecPlan &pl) {
+                         const std::vector<uint32_t> *el_ref, RecPlan &pl, const std::vector<uint32_t> *el_exact) {
     int e = build_decode_plan(c);
     if (e) return e;
     if (!c->dec_ok) return RS_ERR_PANIC;
     const int k = c->k, p = c->p, m = c->m, n = c->n, total = c->total;
     std::vector<uint8_t> erased(total);
     for (int i = 0; i < total; i++) erased[i] = !present[i];
-    const std::vector<uint32_t> *elp = el_ref ? el_ref : error_locs_cached(c, erased);
+    const std::vector<uint32_t> *elp = el_ref ? el_ref : el_exact ? el_exact : error_locs_cached(c, erased);
     if (!elp) return RS_ERR_PANIC;
     const std::vector<uint32_t> &el = *elp;
     // work rows: [recovery m][original k][zero to n] (leopard16.go:547)
@@ -911,8 +924,11 @@ void set_big_sub(const rs_codec *c, RecArgs &ra) {
 }
 
 // Device-resident plan for (present, recover_all), built and uploaded on first use.
-int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, uint64_t S, DevPlan **out) {
-    const std::vector<uint32_t> *el_ref = ref_inv_errlocs(c, present, recover_all, S);
+int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, uint64_t S, DevPlan **out,
+             const ElExt *el_ext = nullptr) {
+    const std::vector<uint32_t> *el_ref =
+        el_ext ? (el_ext->ref ? el_ext->el : nullptr) : ref_inv_errlocs(c, present, recover_all, S);
+    const std::vector<uint32_t> *el_exact = el_ext && !el_ext->ref ? el_ext->el : nullptr;
     std::vector<uint8_t> key = plan_key(present, recover_all, el_ref);
     for (auto it = c->dplan_cache.begin(); it != c->dplan_cache.end(); ++it) {
         if (it->first == key) {
@@ -922,7 +938,7 @@ int dev_plan(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all,
         }
     }
     auto dp = std::make_unique<DevPlan>();
-    if (int e = plan_reconstruct_el(c, present, recover_all, el_ref, dp->pl)) return e;
+    if (int e = plan_reconstruct_el(c, present, recover_all, el_ref, dp->pl, el_exact)) return e;
     const RecPlan &pl = dp->pl;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t s_in = pl.tw_in.size() * 4, s_out = pl.tw_out.size() * 4, s_pos = std::max<size_t>(pl.pos.size(), 1) * 4;
@@ -1189,25 +1205,33 @@ int copy_rows(uint8_t *dev, uint64_t dpitch, uint8_t *const *host, const std::ve
 // when every row of `rows` lies in pinned host memory the device maps
 // (rs_host_alloc, hipHostMalloc), with its device address in z.host[i].  Rows
 // in pageable memory, or registered without a device mapping, keep the copies.
-bool zc_rows(uint8_t *const *shards, const std::vector<int> &rows, ZcRows &z) {
-    if (rows.size() > (size_t)kZcMax) return false;
+// Both ends of each row are looked up: a row whose last byte (S - 1 past its
+// start) is not mapped, or not mapped contiguously with its first (a region
+// registered shorter than the row, or a row spanning two allocations), keeps
+// the copies too, which report an error instead of faulting the GPU.
+bool zc_rows(uint8_t *const *shards, const std::vector<int> &rows, uint64_t S, ZcRows &z) {
+    if (rows.size() > (size_t)kZcMax || S == 0) return false;
     z.n = 0;
-    for (int r : rows) {
-        if ((uintptr_t)shards[r] & 15) return false;  // the kernel moves 16-byte words
+    auto dev_addr = [](const uint8_t *h, uint8_t *&d) {
         hipPointerAttribute_t at{};
-        if (hipPointerGetAttributes(&at, shards[r]) != hipSuccess) {
+        if (hipPointerGetAttributes(&at, h) != hipSuccess) {
             (void)hipGetLastError();
             return false;
         }
         if (at.type != hipMemoryTypeHost || !at.devicePointer || !at.hostPointer) return false;
-        z.host[z.n] = (uint8_t *)at.devicePointer + (shards[r] - (uint8_t *)at.hostPointer);
+        d = (uint8_t *)at.devicePointer + (h - (const uint8_t *)at.hostPointer);
+        return true;
+    };
+    for (int r : rows) {
+        if ((uintptr_t)shards[r] & 15) return false;  // the kernel moves 16-byte words
+        uint8_t *d0 = nullptr, *d1 = nullptr;
+        if (!dev_addr(shards[r], d0) || !dev_addr(shards[r] + (S - 1), d1) || d1 != d0 + (S - 1)) return false;
+        z.host[z.n] = d0;
         z.slab_row[z.n] = (uint16_t)r;
         z.n++;
     }
     return true;
 }
-
-enum class HostOp { Encode, Verify, Reconstruct };
 
 // True when `p` is ordinary pageable host memory (not hipHostMalloc'd or
 // registered).  Device-to-host copies into such memory are staged by the
@@ -1268,7 +1292,7 @@ struct PipeDrainIf {
 // returns after queueing every segment; *ticket completes when the parity is
 // in the caller's rows (rs_encode_wait).
 int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, const std::vector<uint8_t> &present,
-                  bool recover_all, int *ok, uint64_t *ticket = nullptr) {
+                  bool recover_all, int *ok, uint64_t *ticket = nullptr, const ElExt *el_ext = nullptr) {
     int e = ensure_host_pipe(c);
     if (e) return e;
     PipeDrainIf drain_guard{c};
@@ -1285,11 +1309,11 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     if (op == HostOp::Reconstruct) {
         if (int be = build_decode_plan(c)) return be;
         if (c->dec_ok && rec_lds_ok(c)) {
-            e = dev_plan(c, present, recover_all, S, &dpl);
+            e = dev_plan(c, present, recover_all, S, &dpl, el_ext);
             if (e) return e;
             pl = dpl->pl;
         } else {
-            e = plan_reconstruct(c, present, recover_all, S, pl);
+            e = plan_reconstruct(c, present, recover_all, S, pl, el_ext);
             if (e) return e;
         }
         for (int i = 0; i < total; i++)
@@ -1332,8 +1356,8 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     // (30 runs and 32 single rows per segment at C4's random erasures)
     ZcRows zin{}, zout{};
     const int zm = op == HostOp::Reconstruct && !use_bounce ? zc_mask() : 0;
-    const bool zc_in = (zm & 1) && zc_rows(shards, in_rows, zin);
-    const bool zc_out = (zm & 2) && zc_rows(shards, out_rows, zout);
+    const bool zc_in = (zm & 1) && zc_rows(shards, in_rows, S, zin);
+    const bool zc_out = (zm & 2) && zc_rows(shards, out_rows, S, zout);
     std::vector<std::vector<uint8_t *>> btab(kHostBufs, std::vector<uint8_t *>(total));
     if (use_bounce) {
         const size_t need = (size_t)kHostBufs * slab;
@@ -1458,6 +1482,33 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
 }
 
 }  // namespace
+
+// ---------------------------------------------------------------- multi-device parts (multi.hpp)
+int rs::part_host_call(rs_codec *c, HostOp op, uint8_t *const *shards, uint64_t S, const std::vector<uint8_t> &present,
+                       bool recover_all, int *ok, uint64_t *ticket, const ElExt *el) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (int ie = ensure_device(c)) return ie;
+    return host_pipeline(c, shards, S, op, present, recover_all, ok, ticket, el);
+}
+
+// The locators a single-device codec would use for this call (its reference-
+// keyed GF(2^8) cache, whose useBits key depends on the full S, else the exact
+// ones), looked up once per call like leopard8.go:509-554.  The pointer stays
+// valid while the parent's mutex is held, i.e. for the whole multi call.
+int rs::parent_error_locators(rs_codec *c, const std::vector<uint8_t> &present, bool recover_all, uint64_t S,
+                              ElExt &out) {
+    out = ElExt{};
+    if (const std::vector<uint32_t> *r = ref_inv_errlocs(c, present, recover_all, S)) {
+        out.el = r;
+        out.ref = true;
+        return RS_OK;
+    }
+    std::vector<uint8_t> erased(c->total);
+    for (int i = 0; i < c->total; i++) erased[i] = !present[i];
+    out.el = error_locs_cached(c, erased);
+    return out.el ? RS_OK : RS_ERR_PANIC;
+}
 
 // Host simulation of the split schedules against the plain op lists on random
 // GF(2^16) symbols and random twiddle logs (modulus included): returns the
@@ -1637,6 +1688,61 @@ int rs_new(int field_bits, int data_shards, int parity_shards, int device, rs_co
 
 void rs_free(rs_codec *c) { delete c; }
 
+int rs_new_multi(int field_bits, int data_shards, int parity_shards, const int *devices, int ndevices, rs_codec **out) {
+    if (!out) return RS_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!devices || ndevices < 1 || ndevices > RS_MAX_DEVICES) return RS_ERR_INVALID_ARG;
+    rs_codec *c = nullptr;
+    int e = rs_new(field_bits, data_shards, parity_shards, devices[0], &c);
+    if (e) return e;
+    if (ndevices == 1) {  // one device: the plain codec
+        *out = c;
+        return RS_OK;
+    }
+    std::vector<rs_codec *> parts;
+    for (int g = 0; g < ndevices && !e; g++) {
+        rs_codec *q = nullptr;
+        e = rs_new(c->bits, data_shards, parity_shards, devices[g], &q);
+        if (e) break;
+        q->ref_inv = false;  // the parent hands every part its locators (parent_error_locators)
+        parts.push_back(q);
+    }
+    if (!e) {
+        c->multi = multi_create(parts, std::vector<int>(devices, devices + ndevices));
+        if (!c->multi) e = RS_ERR_NOMEM;
+    }
+    if (e) {
+        if (!c->multi)
+            for (rs_codec *q : parts) delete q;
+        delete c;
+        return e;
+    }
+    *out = c;
+    return RS_OK;
+}
+
+int rs_device_count(const rs_codec *c) { return !c ? 0 : c->multi ? multi_count(c->multi) : 1; }
+
+int rs_device_part(rs_codec *c, int index, rs_codec **part, int *device) {
+    if (!c || !part) return RS_ERR_INVALID_ARG;
+    *part = nullptr;
+    if (index < 0 || index >= rs_device_count(c)) return RS_ERR_INVALID_ARG;
+    int dev = c->device;
+    *part = c->multi ? multi_part(c->multi, index, &dev) : c;
+    if (device) *device = dev;
+    return RS_OK;
+}
+
+int rs_byte_range(size_t shard_size, int index, int nparts, size_t *lo, size_t *hi) {
+    if (!lo || !hi || nparts < 1 || index < 0 || index >= nparts) return RS_ERR_INVALID_ARG;
+    if (shard_size % 64) return RS_ERR_INVALID_SHARD_SIZE;
+    uint64_t l = 0, h = 0;
+    part_byte_range(shard_size, index, nparts, l, h);
+    *lo = (size_t)l;
+    *hi = (size_t)h;
+    return RS_OK;
+}
+
 int rs_field_bits(const rs_codec *c) { return c ? c->bits : 0; }
 int rs_data_shards(const rs_codec *c) { return c ? c->k : 0; }
 int rs_parity_shards(const rs_codec *c) { return c ? c->p : 0; }
@@ -1646,6 +1752,7 @@ const char *rs_encode_path(const rs_codec *c) { return c ? c->path.c_str() : "";
 
 int rs_encode_dev(rs_codec *c, uint8_t *const *d, size_t S, void *stream) {
     if (!c || !d) return RS_ERR_INVALID_ARG;
+    if (c->multi) return RS_ERR_INVALID_ARG;  // device rows live on one device: use rs_device_part
     for (int i = 0; i < c->total; i++)
         if (!d[i]) return RS_ERR_INVALID_ARG;
     if (S == 0) return RS_ERR_SHARD_NO_DATA;
@@ -1670,6 +1777,7 @@ int rs_encode_dev(rs_codec *c, uint8_t *const *d, size_t S, void *stream) {
 int rs_encode_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size_t stripe_stride, int nstripes, size_t S,
                         void *stream) {
     if (!c || !base || nstripes <= 0) return RS_ERR_INVALID_ARG;
+    if (c->multi) return RS_ERR_INVALID_ARG;  // device rows live on one device: use rs_device_part
     if (S == 0) return RS_ERR_SHARD_NO_DATA;
     if (S % 64) return RS_ERR_INVALID_SHARD_SIZE;
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1689,6 +1797,7 @@ int rs_encode_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size_t st
 
 int rs_verify_dev(rs_codec *c, uint8_t *const *d, size_t S, int *ok, void *stream) {
     if (!c || !d || !ok) return RS_ERR_INVALID_ARG;
+    if (c->multi) return RS_ERR_INVALID_ARG;  // device rows live on one device: use rs_device_part
     *ok = 0;
     for (int i = 0; i < c->total; i++)
         if (!d[i]) return RS_ERR_INVALID_ARG;
@@ -1717,6 +1826,7 @@ int rs_verify_dev(rs_codec *c, uint8_t *const *d, size_t S, int *ok, void *strea
 int rs_verify_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size_t stripe_stride, int nstripes, size_t S,
                         int *ok, void *stream) {
     if (!c || !base || !ok || nstripes <= 0) return RS_ERR_INVALID_ARG;
+    if (c->multi) return RS_ERR_INVALID_ARG;  // device rows live on one device: use rs_device_part
     *ok = 0;
     if (S == 0) return RS_ERR_SHARD_NO_DATA;
     if (S % 64) return RS_ERR_INVALID_SHARD_SIZE;
@@ -1741,6 +1851,7 @@ int rs_verify_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size_t st
 int rs_reconstruct_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size_t stripe_stride, size_t nstripes,
                              const uint8_t *present, size_t S, int recover_all, void *stream) {
     if (!c || !base || !present || nstripes == 0 || nstripes > (size_t)INT32_MAX) return RS_ERR_INVALID_ARG;
+    if (c->multi) return RS_ERR_INVALID_ARG;  // device rows live on one device: use rs_device_part
     std::vector<uint8_t> pr(present, present + c->total);
     int np = 0, dp = 0;
     for (int i = 0; i < c->total; i++)
@@ -1778,6 +1889,7 @@ int rs_reconstruct_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size
 int rs_reconstruct_dev(rs_codec *c, uint8_t *const *d, const uint8_t *present, size_t S, int recover_all,
                        void *stream) {
     if (!c || !d || !present) return RS_ERR_INVALID_ARG;
+    if (c->multi) return RS_ERR_INVALID_ARG;  // device rows live on one device: use rs_device_part
     std::vector<uint8_t> pr(present, present + c->total);
     int np = 0, dp = 0;
     for (int i = 0; i < c->total; i++)
@@ -1816,6 +1928,7 @@ int rs_encode(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshar
     for (int i = 0; i < nshards; i++)
         if (!shards[i]) return RS_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
+    if (c->multi) return multi_host(c->multi, c, HostOp::Encode, shards, S, {}, true, nullptr, nullptr);
     DeviceGuard g(c->device);
     if (int ie = ensure_device(c)) return ie;
     return host_pipeline(c, shards, S, HostOp::Encode, {}, true, nullptr);
@@ -1832,6 +1945,7 @@ int rs_encode_async(rs_codec *c, uint8_t *const *shards, const size_t *lens, int
     for (int i = 0; i < nshards; i++)
         if (!shards[i]) return RS_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
+    if (c->multi) return multi_host(c->multi, c, HostOp::Encode, shards, S, {}, true, nullptr, ticket);
     DeviceGuard g(c->device);
     if (int ie = ensure_device(c)) return ie;
     return host_pipeline(c, shards, S, HostOp::Encode, {}, true, nullptr, ticket);
@@ -1839,6 +1953,7 @@ int rs_encode_async(rs_codec *c, uint8_t *const *shards, const size_t *lens, int
 
 int rs_encode_query(rs_codec *c, uint64_t ticket, int *done) {
     if (!c || !done) return RS_ERR_INVALID_ARG;
+    if (c->multi) return multi_ticket_query(c->multi, ticket, done);
     hipEvent_t ev;
     {
         std::lock_guard<std::mutex> lk(c->mu);
@@ -1862,6 +1977,7 @@ int rs_encode_query(rs_codec *c, uint64_t ticket, int *done) {
 
 int rs_encode_wait(rs_codec *c, uint64_t ticket) {
     if (!c) return RS_ERR_INVALID_ARG;
+    if (c->multi) return multi_ticket_wait(c->multi, ticket);
     hipEvent_t ev;
     {
         std::lock_guard<std::mutex> lk(c->mu);
@@ -1890,6 +2006,7 @@ int rs_verify_async(rs_codec *c, uint8_t *const *shards, const size_t *lens, int
     for (int i = 0; i < nshards; i++)
         if (!shards[i]) return RS_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
+    if (c->multi) return multi_host(c->multi, c, HostOp::Verify, shards, S, {}, true, nullptr, ticket);
     DeviceGuard g(c->device);
     if (int ie = ensure_device(c)) return ie;
     return host_pipeline(c, shards, S, HostOp::Verify, {}, true, nullptr, ticket);
@@ -1898,6 +2015,7 @@ int rs_verify_async(rs_codec *c, uint8_t *const *shards, const size_t *lens, int
 int rs_verify_result(rs_codec *c, uint64_t ticket, int *ok) {
     if (!c || !ok) return RS_ERR_INVALID_ARG;
     *ok = 0;
+    if (c->multi) return multi_verify_result(c->multi, ticket, ok);
     const int slot = (int)(ticket % rs_codec::kTickets);
     // the slot must still hold this verify ticket (not reused by a later call)
     auto owns_slot = [&] {
@@ -1929,6 +2047,7 @@ int rs_verify(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshar
     for (int i = 0; i < nshards; i++)
         if (!shards[i]) return RS_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
+    if (c->multi) return multi_host(c->multi, c, HostOp::Verify, shards, S, {}, true, ok, nullptr);
     DeviceGuard g(c->device);
     if (int ie = ensure_device(c)) return ie;
     return host_pipeline(c, shards, S, HostOp::Verify, {}, true, ok);
@@ -1958,11 +2077,15 @@ int reconstruct_host(rs_codec *c, uint8_t *const *shards, size_t *lens, int nsha
     for (int i = 0; i < c->total; i++)
         if ((lens[i] || i < end) && !shards[i]) return RS_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    if (int ie = ensure_device(c)) return ie;
     std::vector<uint8_t> pr(c->total);
     for (int i = 0; i < c->total; i++) pr[i] = lens[i] != 0;
-    e = host_pipeline(c, shards, S, HostOp::Reconstruct, pr, recover_all != 0, nullptr, ticket);
+    if (c->multi) {
+        e = multi_host(c->multi, c, HostOp::Reconstruct, shards, S, pr, recover_all != 0, nullptr, ticket);
+    } else {
+        DeviceGuard g(c->device);
+        if (int ie = ensure_device(c)) return ie;
+        e = host_pipeline(c, shards, S, HostOp::Reconstruct, pr, recover_all != 0, nullptr, ticket);
+    }
     if (e) return e;
     for (int i = 0; i < end; i++)
         if (!pr[i]) lens[i] = S;
@@ -1992,6 +2115,7 @@ int rs_split_shard_size(const rs_codec *c, size_t len, size_t *per_shard) {
 
 int rs_split(rs_codec *c, const uint8_t *data, size_t len, uint8_t *dst, size_t dst_stride, void *stream) {
     if (!c || !data || !dst) return RS_ERR_INVALID_ARG;
+    if (c->multi) c = multi_part(c->multi, 0, nullptr);  // same geometry; device copies on part 0's stream
     if (len == 0) return RS_ERR_SHORT_DATA;  // leopard16.go:279-281
     const size_t per = split_per_shard(c, len);
     if (dst_stride < per && c->total > 1) return RS_ERR_INVALID_ARG;
@@ -2029,6 +2153,7 @@ int rs_split(rs_codec *c, const uint8_t *data, size_t len, uint8_t *dst, size_t 
 int rs_join(rs_codec *c, uint8_t *const *shards, const size_t *lens, int nshards, uint8_t *dst, size_t out_size,
             void *stream) {
     if (!c || !shards || !lens || (!dst && out_size)) return RS_ERR_INVALID_ARG;
+    if (c->multi) c = multi_part(c->multi, 0, nullptr);
     if (nshards < c->k) return RS_ERR_TOO_FEW_SHARDS;  // leopard16.go:232-236
     size_t size = 0;
     int use = 0;
@@ -2067,6 +2192,7 @@ int rs_set_host_segment(rs_codec *c, size_t bytes) {
     if (!c || bytes % 64) return RS_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     c->host_seg_bytes = bytes;
+    if (c->multi) return multi_set_host_segment(c->multi, bytes);
     return RS_OK;
 }
 

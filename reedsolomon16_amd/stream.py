@@ -329,8 +329,22 @@ class _StreamCodec:
 
             self._pool = ThreadPoolExecutor(max_workers=threads)
 
-    def _each(self, jobs) -> None:
-        """Run every job; re-raise the lowest-index job's exception."""
+    def close(self) -> None:
+        """Shut the read/write thread pool down and drop the block buffers."""
+        pool, self._pool = self._pool, None
+        if pool is not None:
+            pool.shutdown(wait=True)
+        self._bufs = None
+
+    def _each(self, jobs, objs=None) -> None:
+        """Run every job; re-raise the lowest-index job's exception.  `objs`
+        are the readers / writers the jobs use: when one object appears twice
+        (an aliased reader), the jobs run one after another in index order, so
+        it sees its bytes in the order of the reference's sequential loop."""
+        if objs is not None and len({id(o) for o in objs}) < len(objs):
+            for j in jobs:
+                j()
+            return
         if self._pool is None or len(jobs) < 2:
             for j in jobs:
                 j()
@@ -366,7 +380,7 @@ class _StreamCodec:
                     raise StreamReadError(e, i) from e
             return run
 
-        self._each([job(i, rd) for i, rd in enumerate(readers) if rd is not None])
+        self._each([job(i, rd) for i, rd in enumerate(readers) if rd is not None], [rd for rd in readers if rd is not None])
         lens.extend(got)
         return next((n for n in got if n > 0), -1)
 
@@ -401,7 +415,7 @@ class _StreamCodec:
             t.wait()
             al = _ceil64(size)  # writeOutputs (streaming16.go:173-197, streaming8.go:318-340)
             self._each([(lambda w=w, j=j: _write(w, rows[self.k + j][:al], self.k + j))
-                        for j, w in enumerate(outputs) if w is not None])
+                        for j, w in enumerate(outputs) if w is not None], [w for w in outputs if w is not None])
 
         blk = 0
         try:
@@ -531,7 +545,7 @@ class _StreamCodec:
         def drain_one():
             t, blk_shards, size, al = pending.popleft()
             t.wait()
-            jobs = []
+            jobs, objs = [], []
             for i, w in enumerate(outputs):
                 if w is None or not missing[i]:
                     continue
@@ -542,7 +556,8 @@ class _StreamCodec:
                 else:
                     ws = size if i < self.k else al  # streaming16.go:445-464
                 jobs.append(lambda w=w, i=i, ws=ws: _write(w, np.asarray(blk_shards[i])[:ws], i))
-            self._each(jobs)
+                objs.append(w)
+            self._each(jobs, objs)
 
         blk, read = 0, 0
         try:
@@ -643,5 +658,5 @@ class StreamEncoder8(_StreamCodec):
             t.wait()
             read += size
             self._each([(lambda w=w, i=i: _write(w, rows[i][:size if i < self.k else al], i))
-                        for i, w in enumerate(outputs) if w is not None])
+                        for i, w in enumerate(outputs) if w is not None], [w for w in outputs if w is not None])
             blk += 1

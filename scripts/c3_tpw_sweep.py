@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--tails", default="-1", help="hp_tail values of a lab build (single-tile tail; -1 = the product, no knob)")
     ap.add_argument("--alloc", type=int, default=0, help="stripes to allocate (0: the largest launched)")
     ap.add_argument("--geom", default="128,32")
-    ap.add_argument("--pad", type=int, default=3584, help="bytes between rows beyond the row (0: rows back to back)")
+    ap.add_argument("--pad", default="3584", help="bytes between rows beyond the row (0: rows back to back); a comma list sweeps")
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     import torch
@@ -30,15 +30,16 @@ def main():
     from reedsolomon16_amd import dist as rsd
 
     K, P = (int(x) for x in a.geom.split(","))
-    S, pad = 1 << 20, a.pad
+    S = 1 << 20
+    pads = [int(x) for x in a.pad.split(",")]
     codec = rs.New16(K, P)
     bmax = a.alloc or max(int(x) for x in a.stripes.split(","))
     for nsl in (int(x) for x in a.slices.split(",")):
         lo, hi = rsd.byte_range(S, 0, nsl)
         W = hi - lo
-        RS = W + pad
-        buf = torch.randint(0, 256, (bmax * (K + P) * RS,), dtype=torch.uint8, device="cuda")
-        for B in (int(x) for x in a.stripes.split(",")):
+        buf = torch.randint(0, 256, (bmax * (K + P) * (W + max(pads)),), dtype=torch.uint8, device="cuda")
+        for B, pad in [(int(x), pd) for x in a.stripes.split(",") for pd in pads]:
+            RS = W + pad
             slab = buf[: B * (K + P) * RS].as_strided((B, K + P, W), ((K + P) * RS, RS, 1))
             for t, stp, tl in [(int(x), int(y), int(z)) for x in a.tiles.split(",") for y in a.steps.split(",") for z in a.tails.split(",")]:
                 if t == 1 and (stp or tl > 0):

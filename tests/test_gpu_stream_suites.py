@@ -37,7 +37,7 @@ def test_gpu_reference_stream_suite_case(case):
 
 
 def test_gpu_stream_methods_reuse_one_stream_codec():
-    """Stream* calls on one codec share its pinned block buffers; a GF(2^8)
+    """Stream* calls on one codec reuse its pinned block buffers; a GF(2^8)
     codec's streams run on a codec of their own (fresh inversion cache per
     call, reedsolomon.go:132), a GF(2^16) codec's on itself."""
     c16 = rs.New16(4, 2)
@@ -45,14 +45,68 @@ def test_gpu_stream_methods_reuse_one_stream_codec():
     try:
         case = "StreamVerify/FF16_Size_32768"
         ref_suites.run(c16, case)
-        s = c16._stream()
+        with c16._stream() as s:
+            pass
         ref_suites.run(c16, case)
-        assert c16._stream() is s and s.rs is c16
+        with c16._stream() as s2:
+            assert s2 is s and s.rs is c16
+            # a call while the kept one is busy gets a fresh stream codec
+            with c16._stream() as s3:
+                assert s3 is not s and s3.rs is c16
         ref_suites.run(c8, "StreamVerify/FF8_Size_32768")
-        assert c8._stream().rs is not c8 and c8._stream().rs.field_bits == 8
+        with c8._stream() as s8:
+            assert s8.rs is not c8 and s8.rs.field_bits == 8
     finally:
         c16.close()
         c8.close()
+
+
+def test_gpu_stream_calls_from_two_threads():
+    """Concurrent StreamEncode calls on one codec (advisor finding, round 5):
+    each call has block buffers of its own, so both streams' parity is exact."""
+    import io
+    import threading
+
+    import numpy as np
+
+    from oracle import orc
+
+    k, p, n = 6, 3, (4 << 20) * 2 + 4096  # two 4 MiB blocks and a short one per shard
+    c = rs.New16(k, p)
+    rng = np.random.default_rng(9)
+    datas = [rng.integers(0, 256, (k, n), dtype=np.uint8) for _ in range(2)]
+    outs = [[io.BytesIO() for _ in range(p)] for _ in range(2)]
+    errs = []
+
+    def run(j):
+        try:
+            for _ in range(2):
+                for o in outs[j]:
+                    o.seek(0)
+                    o.truncate()
+                c.stream_encode([io.BytesIO(datas[j][i].tobytes()) for i in range(k)], outs[j])
+        except Exception as e:
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(j,)) for j in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    try:
+        for j in range(2):
+            for off in (0, 4 << 20, 8 << 20):
+                w = min(4 << 20, n - off)
+                al = (w + 63) // 64 * 64
+                blk = np.zeros((k, al), np.uint8)
+                blk[:, :w] = datas[j][:, off:off + w]
+                ref = orc.encode(16, k, p, blk)
+                for i in range(p):
+                    got = np.frombuffer(outs[j][i].getvalue(), np.uint8)
+                    assert np.array_equal(got[off:off + al], ref[i]), (j, off, i)
+    finally:
+        c.close()
 
 
 def test_gpu_with_concurrency_returns_the_codec():

@@ -517,3 +517,27 @@ def test_stream_threads_report_the_lowest_failing_reader():
     with pytest.raises(StreamReadError) as ei:
         st.encode(rd, [io.BytesIO() for _ in range(p)])
     assert ei.value.stream == 2
+
+
+def test_stream_threads_aliased_reader_reads_in_order():
+    """One reader object passed for several shards (advisor finding, round 5):
+    with threads > 1 the mirror reads it in index order, as the reference's
+    sequential loop does, so every shard gets the same bytes as threads = 1."""
+    k, p = 6, 3
+    payload = bytes(range(256)) * 40
+    outs = []
+    for threads in (1, 4):
+        st, _ = _mirror_threads(k, p, 16, threads)
+        shared = io.BytesIO(payload)
+        mout = [io.BytesIO() for _ in range(p)]
+        st.encode([shared] * k, mout)
+        outs.append([o.getvalue() for o in mout])
+        st.close()
+    assert outs[0] == outs[1]
+
+
+def test_stream_close_shuts_the_pool_down():
+    st, _ = _mirror_threads(4, 2, 16, 4)
+    pool = st._pool
+    st.close()
+    assert st._pool is None and pool._shutdown
