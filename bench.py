@@ -255,23 +255,34 @@ def c2_encode(torch, rs, dev, stream) -> dict:
     k, p, S = 10, 4, 1 << 20
     g = torch.Generator(device=dev)
     g.manual_seed(0xC2)
+    import time
+
+    from reedsolomon16_amd.codec import _stream_handle
+
     c2 = rs.New8(k, p, device=dev.index)
     slab = torch.randint(0, 256, (16, k + p, S), dtype=torch.uint8, device=dev, generator=g)
-    out = {"config": "10+4 x 1024 KiB, GF(2^8)", "kernel_path": c2.encode_path}
+    out = {"config": "10+4 x 1024 KiB, GF(2^8)", "kernel_path": c2.encode_path,
+           "caller": "rs_encode_dev_batch through ctypes with prebuilt arguments (a C or cgo caller's "
+                     "per-call cost; the Python wrapper's own argument checks are not timed)"}
+    fn = rs.lib().rs_encode_dev_batch
     for ns, reps in ((1, 400), (16, 100)):
         view = slab[:ns]
+        args = (c2._h, view.data_ptr(), view.stride(1), view.stride(0), ns, S, _stream_handle(stream))
         for _ in range(10):
-            c2.encode_dev_batch(view, stream)
+            assert fn(*args) == 0
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         e0.record(stream)
+        t0 = time.perf_counter()
         for _ in range(reps):
-            c2.encode_dev_batch(view, stream)
+            fn(*args)
+        t1 = time.perf_counter()
         e1.record(stream)
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
         alg = ns * (k + p) * S
         out[f"stripes_{ns}"] = {"kernel_ms": round(ms, 5), "us_per_stripe": round(ms * 1e3 / ns, 3),
+                                "host_us_per_call": round((t1 - t0) * 1e6 / reps, 3),
                                 "alg_bytes_per_launch": alg,
                                 "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
     del slab
@@ -368,17 +379,29 @@ def host_resident(rs, blocks: int = 2, block: int = 4 << 20) -> dict:
         for t in ts:
             t.wait()
 
-    tick = {}
-    for name, fn, rd, wr in (("encode", enc, K, P), ("verify", ver, K + P, 0),
-                             ("reconstruct", rec, K + P - len(erased), len(erased))):
-        fn()  # warm: plans, staging buffers
-        t0 = time.perf_counter()
-        fn()
-        tick[name] = rate(name, time.perf_counter() - t0, rd, wr)
-    for j, i in enumerate(erased):
-        src = data[i] if i < K else par[i - K]
-        assert all(np.array_equal(rebuilt[b, j], src[b * block:(b + 1) * block]) for b in range(blocks))
-    out["tickets"] = tick
+    def tickets():
+        tick = {}
+        for name, fn, rd, wr in (("encode", enc, K, P), ("verify", ver, K + P, 0),
+                                 ("reconstruct", rec, K + P - len(erased), len(erased))):
+            fn()  # warm: plans, staging buffers
+            t0 = time.perf_counter()
+            fn()
+            tick[name] = rate(name, time.perf_counter() - t0, rd, wr)
+        for j, i in enumerate(erased):
+            src = data[i] if i < K else par[i - K]
+            assert all(np.array_equal(rebuilt[b, j], src[b * block:(b + 1) * block]) for b in range(blocks))
+        return tick
+
+    out["tickets"] = tickets()
+    # the same tickets on a multi-device codec of four parts on this one GPU
+    # (rs_new_multi, devices = [d, d, d, d]): the cost of the byte-range
+    # fan-out over per-part host threads and streams, sharing one PCIe link
+    # (an 8-GPU node's parts each own a link; not measurable on this box)
+    one = codec
+    codec = rs.New16(K, P, devices=[one.device] * 4)
+    out["tickets_parts4_one_gpu"] = tickets()
+    codec.close()
+    codec = one
 
     # ---- the rsStream16 mirror over readers / writers: the reference's
     # sequential loops, and the same loops with a block's readers and writers

@@ -293,6 +293,8 @@ int rs_debug_dec_plan(int mtrunc, const uint32_t *need, uint64_t *code);
  *   "unit_width" -1/0/1  LDS and GF(2^8) register units automatic / wide / narrow (default -1),
  *   "hp_tiles" 0..64  bit-sliced encode tiles per workgroup, 0 = automatic (default 0),
  *   "hp_step" >= 0    distance in tiles between a workgroup's tiles, 0 = the grid size (default 0),
+ *   "hp_tune" 0/1     run-time choice of the bit-sliced encode's tile map by timing both
+ *                     on the first launches of a shape (default 1; 0: the static rule),
  *   "zc"      0..3    host reconstruct over pinned mapped rows: zero-copy kernels move the
  *                     present rows in (bit 0) and the rebuilt rows out (bit 1) (default 3);
  *                     a cleared bit keeps that direction's per-run hipMemcpy copies.

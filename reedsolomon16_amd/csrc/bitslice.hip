@@ -48,7 +48,10 @@
 // are in-place inline asm so the compiler cannot rename their intermediates
 // into fresh registers, and every butterfly is a scheduling region.
 #include <algorithm>
+#include <array>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <utility>
 
 #include "bs_common.hpp"
@@ -404,6 +407,63 @@ __global__ void __launch_bounds__(256, kHpWgPerCu<LOGM>) k_encode_hp(BsArgs a) {
     e.run();
 }
 
+// Run-time choice of the tile map for launches where both maps are candidates
+// (four tiles per workgroup a grid apart, or one).  Which one wins depends on
+// the box: four tiles gave 0.683-0.686 against 0.655 for one on three boxes
+// of round 6 and 0.634 against 0.657 on a fourth (full 1 MiB rows, 256
+// stripes; profiles/r06_c3_tile_map_boxes.txt), with the same code and
+// launch.  So the first launches of a shape alternate the two maps under
+// events on the launch stream, and once kTrials of them have completed the
+// shape keeps the map with the smaller median (the first pair, cold, is
+// dropped).  Until then, and after a tie, the static rule's four tiles run.
+// Both maps compute the same bytes (test_bs_tiles_per_workgroup).
+class HpTuner {
+  public:
+    static constexpr int kTrials = 8;
+    typedef std::array<int64_t, 8> Key;  // device, logm, verify, ntiles, tiles per stripe, strides, S
+    // tpw for this launch; *e0 / *e1 events to record around it (trial launches only)
+    int choose(const Key &key, hipEvent_t *e0, hipEvent_t *e1) {
+        std::lock_guard<std::mutex> lk(mu_);
+        Entry &t = m_[key];
+        if (t.pick) return t.pick;
+        if (t.n < kTrials) {
+            if (hipEventCreate(&t.ev[t.n][0]) != hipSuccess || hipEventCreate(&t.ev[t.n][1]) != hipSuccess) {
+                t.pick = kMany;  // no events: keep the static rule
+                return t.pick;
+            }
+            *e0 = t.ev[t.n][0];
+            *e1 = t.ev[t.n][1];
+            return t.n++ % 2 ? 1 : kMany;
+        }
+        if (hipEventQuery(t.ev[kTrials - 1][1]) != hipSuccess) return kMany;  // trials still running
+        float ms[2][kTrials / 2 - 1];
+        bool ok = true;
+        for (int i = 2; i < kTrials; i++)
+            ok = ok && hipEventElapsedTime(&ms[i % 2][i / 2 - 1], t.ev[i][0], t.ev[i][1]) == hipSuccess;
+        for (auto &e : t.ev) {
+            (void)hipEventDestroy(e[0]);
+            (void)hipEventDestroy(e[1]);
+        }
+        auto med = [](float *x) {
+            std::sort(x, x + kTrials / 2 - 1);
+            return x[(kTrials / 2 - 1) / 2];
+        };
+        t.pick = ok && med(ms[1]) < med(ms[0]) ? 1 : kMany;
+        if (m_.size() > 256) m_.clear();  // shapes of a long-lived process: re-tune rather than grow
+        return t.pick;
+    }
+    static constexpr int kMany = 4;
+
+  private:
+    struct Entry {
+        int n = 0, pick = 0;
+        hipEvent_t ev[kTrials][2] = {};
+    };
+    std::mutex mu_;
+    std::map<Key, Entry> m_;
+};
+HpTuner g_hp_tuner;
+
 template <int LOGM>
 hipError_t launch_hp_t(bool verify, BsArgs a, int cus, hipStream_t s) {
     a.tiles_per_stripe = (int)((a.S + 2047) / 2048);
@@ -427,8 +487,15 @@ hipError_t launch_hp_t(bool verify, BsArgs a, int cus, hipStream_t s) {
     // r05_c3_tiles_per_wg.txt, calls r5h, r5k, r5m).
     const int slots = std::max(cus, 1) * kHpWgPerCu<LOGM>;
     int tpw = hp_tiles_override();
-    if (tpw <= 0)
-        tpw = (a.ntiles >= 224 * slots || (a.tiles_per_stripe <= 256 && a.ntiles >= 32 * slots)) ? 4 : 1;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (tpw <= 0) {
+        tpw = (a.ntiles >= 224 * slots || (a.tiles_per_stripe <= 256 && a.ntiles >= 32 * slots)) ? HpTuner::kMany : 1;
+        int dev = 0;
+        if (tpw > 1 && hp_tune_enabled() && hipGetDevice(&dev) == hipSuccess)
+            tpw = g_hp_tuner.choose({dev, LOGM, verify ? 1 : 0, a.ntiles, a.tiles_per_stripe, (int64_t)a.row_stride,
+                                     a.nstripes > 1 ? (int64_t)a.stripe_stride : 0, (int64_t)a.S},
+                                    &e0, &e1);
+    }
     int step = hp_step_override();
     if (step <= 0) step = (a.ntiles + tpw - 1) / tpw;
     step = std::min(step, a.ntiles);
@@ -437,9 +504,12 @@ hipError_t launch_hp_t(bool verify, BsArgs a, int cus, hipStream_t s) {
     const int grid = blocks * step + std::min(rem, step);
     a.tpw = tpw;
     a.tile_step = step;
+    if (e0) (void)hipEventRecord(e0, s);
     if (verify) hipLaunchKernelGGL((k_encode_hp<LOGM, true>), dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_encode_hp<LOGM, false>), dim3(grid), dim3(256), 0, s, a);
-    return hipGetLastError();
+    const hipError_t le = hipGetLastError();
+    if (e1) (void)hipEventRecord(e1, s);
+    return le;
 }
 
 int hp_logm(int p) { return p > 16 ? 5 : 4; }

@@ -349,7 +349,7 @@ int upload_split(rs_codec *c) {
 // the reconstruct FFT unpruned, the narrow / wide LDS units) on the same small
 // inputs.  Process-wide; read when a codec is created (bs) or at each launch.
 std::atomic<int> g_path_bs{1}, g_path_sub{1}, g_path_prune{1}, g_path_unit_width{-1}, g_path_hp_tiles{0}, g_path_hp_step{0},
-    g_path_zc{3};
+    g_path_zc{3}, g_path_hp_tune{1};
 bool bs_enabled() { return g_path_bs.load(std::memory_order_relaxed) != 0; }
 bool sub_enabled() { return g_path_sub.load(std::memory_order_relaxed) != 0; }
 bool prune_enabled() { return g_path_prune.load(std::memory_order_relaxed) != 0; }
@@ -358,6 +358,7 @@ int zc_mask() { return g_path_zc.load(std::memory_order_relaxed); }
 int rs::unit_width_override() { return g_path_unit_width.load(std::memory_order_relaxed); }
 int rs::hp_tiles_override() { return g_path_hp_tiles.load(std::memory_order_relaxed); }
 int rs::hp_step_override() { return g_path_hp_step.load(std::memory_order_relaxed); }
+bool rs::hp_tune_enabled() { return g_path_hp_tune.load(std::memory_order_relaxed) != 0; }
 namespace {
 
 // Host half of the encode plan (no device calls): twiddle schedule and panic check.
@@ -534,6 +535,13 @@ int scratch_acquire(rs_codec *c, hipStream_t s) {
 int scratch_host_wait(rs_codec *c) {
     if (c->scratch_used) HIP_TRY(hipEventSynchronize(c->scratch_ev));
     return RS_OK;
+}
+// Does an encode launch over these row sets touch the codec scratch (the
+// device row table, the multi-pass work rows)?  Launches that do not skip the
+// scratch event: one hipEventRecord less per call (the single-stripe
+// device-resident encode is host-bound).
+bool encode_uses_scratch(const rs_codec *c, const RowSet &data, const RowSet &par) {
+    return data.table || par.table || c->logm > kMaxLdsLogN;
 }
 // Mark the scratch as used by the work queued on `s` so far.
 int scratch_release(rs_codec *c, hipStream_t s) {
@@ -1764,12 +1772,11 @@ int rs_encode_dev(rs_codec *c, uint8_t *const *d, size_t S, void *stream) {
     RowSet data, par;
     int e = make_rowsets(c, d, s, data, par);
     if (e) return e;
-    e = scratch_acquire(c, s);
-    if (e) return e;
+    const bool scr = encode_uses_scratch(c, data, par);
+    if (scr && (e = scratch_acquire(c, s))) return e;
     e = encode_device(c, data, par, S, 0, 1, nullptr, s);
     if (e) return e;
-    e = scratch_release(c, s);
-    if (e) return e;
+    if (scr && (e = scratch_release(c, s))) return e;
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return RS_OK;
 }
@@ -1785,12 +1792,12 @@ int rs_encode_dev_batch(rs_codec *c, uint8_t *base, size_t row_stride, size_t st
     if (int ie = ensure_device(c)) return ie;
     hipStream_t s = pick_stream(c, stream);
     RowSet data{nullptr, base, row_stride}, par{nullptr, base + (size_t)c->k * row_stride, row_stride};
-    int e = scratch_acquire(c, s);
+    const bool scr = encode_uses_scratch(c, data, par);
+    int e = scr ? scratch_acquire(c, s) : RS_OK;
     if (e) return e;
     e = encode_device(c, data, par, S, stripe_stride, nstripes, nullptr, s);
     if (e) return e;
-    e = scratch_release(c, s);
-    if (e) return e;
+    if (scr && (e = scratch_release(c, s))) return e;
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return RS_OK;
 }
@@ -2306,6 +2313,7 @@ int rs_debug_set_path(const char *knob, int value) {
     else if (k == "unit_width" && value >= -1 && value <= 1) g_path_unit_width = value;
     else if (k == "hp_tiles" && value >= 0 && value <= 64) g_path_hp_tiles = value;
     else if (k == "hp_step" && value >= 0) g_path_hp_step = value;
+    else if (k == "hp_tune" && value >= 0 && value <= 1) g_path_hp_tune = value;
     else if (k == "zc" && value >= 0 && value <= 3) g_path_zc = value;
     else return RS_ERR_INVALID_ARG;
     return RS_OK;

@@ -63,6 +63,7 @@ int unit_width_override();
 // and the distance in tiles between a workgroup's tiles, 0 = the grid size.
 int hp_tiles_override();
 int hp_step_override();
+bool hp_tune_enabled();
 
 hipError_t launch_encode_reg(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 // Half-wave split encode (GF(2^16), logm 2..5, strided rows only: data.table ==

@@ -45,6 +45,17 @@ int main() {
                std::chrono::duration<double, std::micro>(t1 - t0).count() / 50, ms * 1e3 / 50);
     };
     probe("rs_encode_dev_batch C5", [&] { rs_encode_dev_batch(c, slab, S, rows * S, 1, S, s); });
+    // C2 (GF(2^8) 10 + 4 x 1 MiB), one stripe per call: the shape every
+    // New(10, 4).Encode of a device-resident stripe produces
+    rs_codec *c2 = nullptr;
+    if (rs_new(8, 10, 4, 0, &c2)) return 1;
+    const size_t S2 = 1 << 20;
+    probe("rs_encode_dev_batch C2 x1", [&] { rs_encode_dev_batch(c2, slab, S2, 14 * S2, 1, S2, s); });
+    probe("rs_encode_dev_batch C2 x16", [&] { rs_encode_dev_batch(c2, slab, S2, 14 * S2, 16, S2, s); });
+    uint8_t *rows2[14];
+    for (int i = 0; i < 14; i++) rows2[i] = slab + i * S2;
+    probe("rs_encode_dev C2 x1 (rows)", [&] { rs_encode_dev(c2, rows2, S2, s); });
+    rs_free(c2);
     probe("k_spin", [&] { hipLaunchKernelGGL(k_spin, dim3((64 << 20) / 256), dim3(256), 0, s, x, 64 << 20, 20); });
     rs_free(c);
     return 0;

@@ -77,6 +77,36 @@ def test_bs_tiles_per_workgroup(torch, paths, tiles, step, k, p, S, n):
     assert not c.verify_dev_batch(slab)
 
 
+def test_bs_tile_map_tuner(torch, paths):
+    """The run-time tile-map choice (launch_hp_t HpTuner): the first launches
+    of a candidate shape alternate four tiles per workgroup and one under
+    events, later ones keep the faster map.  Every launch of the sequence --
+    trials, the decision, the launches after it -- writes the parity one tile
+    per workgroup writes (itself checked against the oracle on a window), and
+    verify agrees.  Shape: the 8-rank slice of C3 (128 KiB of every row, 256
+    stripes: 16384 tiles, both maps candidates)."""
+    k, p, S, n = 128, 32, 128 << 10, 256
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x7A)
+    slab = torch.randint(0, 256, (n, k + p, S), dtype=torch.uint8, device="cuda", generator=g)
+    c = rs.New16(k, p)
+    paths("hp_tiles", 1)
+    c.encode_dev_batch(slab)
+    torch.cuda.synchronize()
+    ref = slab[:, k:].clone()
+    for j in (0, n - 1):
+        d = slab[j, :k, 4096:8192].cpu().numpy()
+        assert np.array_equal(ref[j, :, 4096:8192].cpu().numpy(), orc.encode(16, k, p, np.ascontiguousarray(d)))
+    paths("hp_tiles", 0)
+    paths("hp_tune", 1)
+    for it in range(14):
+        slab[:, k:] = 0
+        c.encode_dev_batch(slab)
+        torch.cuda.synchronize()
+        assert torch.equal(slab[:, k:], ref), f"launch {it}"
+    assert c.verify_dev_batch(slab)
+
+
 @pytest.mark.parametrize("k,p", [(128, 32), (64, 16)])
 def test_bs_special_inputs(torch, k, p):
     """All-zero, all-0xFF and single-symbol impulses in every chunk."""
