@@ -409,10 +409,10 @@ __global__ void __launch_bounds__(256, kHpWgPerCu<LOGM>) k_encode_hp(BsArgs a) {
 
 // Run-time choice of the tile map for launches where both maps are candidates
 // (four tiles per workgroup a grid apart, or one).  Which one wins depends on
-// the box: four tiles gave 0.683-0.686 against 0.655 for one on three boxes
-// of round 6 and 0.634 against 0.657 on a fourth (full 1 MiB rows, 256
-// stripes; profiles/r06_c3_tile_map_boxes.txt), with the same code and
-// launch.  So the first launches of a shape alternate the two maps under
+// the box: four tiles gave 0.684-0.686 against 0.655 for one on two boxes
+// of round 6, and 0.634-0.640 against 0.653-0.657 on two others (full 1 MiB
+// rows, 256 stripes; the 8-rank slice moves the other way on some boxes:
+// profiles/r06_c3_tile_map_boxes.txt), with the same code and launch.  So the first launches of a shape alternate the two maps under
 // events on the launch stream, and once kTrials of them have completed the
 // shape keeps the map with the smaller median (the first pair, cold, is
 // dropped).  Until then, and after a tie, the static rule's four tiles run.
