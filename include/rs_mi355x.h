@@ -285,6 +285,12 @@ int rs_debug_split_emulate(rs_codec *codec, const uint8_t *data, uint8_t *parity
  * Returns 0, or -1 when the kernel does not serve mtrunc.  Host only. */
 int rs_debug_dec_plan(int mtrunc, const uint32_t *need, uint64_t *code);
 
+/* 1 when the host reconstruct would move these rows (S bytes each) with its
+ * zero-copy kernels: every row 16-byte aligned and mapped for the device from
+ * its first to its last byte, contiguously (codec.cpp zc_rows); 0 when it
+ * would copy them.  Pointer queries only, nothing is launched. */
+int rs_debug_zc_rows(uint8_t *const *rows, int nrows, size_t S);
+
 /* Test-only kernel-path overrides (process-wide), so the parity tests can run
  * the variants other geometries select on the same small inputs:
  *   "bs" 0/1          bit-sliced GF(2^16) encode off / on (default 1; read by rs_new),
@@ -295,6 +301,8 @@ int rs_debug_dec_plan(int mtrunc, const uint32_t *need, uint64_t *code);
  *   "hp_step" >= 0    distance in tiles between a workgroup's tiles, 0 = the grid size (default 0),
  *   "hp_tune" 0/1     run-time choice of the bit-sliced encode's tile map by timing both
  *                     on the first launches of a shape (default 1; 0: the static rule),
+ *   "rec_half" 0/1    GF(2^16) reconstruct with n = 1024 / 2048 in 32-byte half tiles, two
+ *                     workgroups per CU (1), or 64-byte tiles, one per CU (0),
  *   "zc"      0..3    host reconstruct over pinned mapped rows: zero-copy kernels move the
  *                     present rows in (bit 0) and the rebuilt rows out (bit 1) (default 3);
  *                     a cleared bit keeps that direction's per-run hipMemcpy copies.

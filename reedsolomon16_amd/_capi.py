@@ -78,11 +78,12 @@ def lib() -> C.CDLL:
     L.rs_debug_sub_swap.restype = C.c_uint32
     L.rs_debug_dec_plan.argtypes = [i32, vp, vp]
     L.rs_debug_set_path.argtypes = [C.c_char_p, i32]
+    L.rs_debug_zc_rows.argtypes = [P(vp), i32, sz]
     _lib = L
     return L
 
 
-_PATH_DEFAULTS = {"bs": 1, "sub": 1, "prune": 1, "unit_width": -1, "hp_tiles": 0, "hp_step": 0, "zc": 3, "hp_tune": 1}
+_PATH_DEFAULTS = {"bs": 1, "sub": 1, "prune": 1, "unit_width": -1, "hp_tiles": 0, "hp_step": 0, "zc": 3, "hp_tune": 1, "rec_half": 0}
 
 
 def set_path(knob: str, value: int) -> None:

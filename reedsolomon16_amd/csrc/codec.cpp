@@ -349,7 +349,7 @@ int upload_split(rs_codec *c) {
 // the reconstruct FFT unpruned, the narrow / wide LDS units) on the same small
 // inputs.  Process-wide; read when a codec is created (bs) or at each launch.
 std::atomic<int> g_path_bs{1}, g_path_sub{1}, g_path_prune{1}, g_path_unit_width{-1}, g_path_hp_tiles{0}, g_path_hp_step{0},
-    g_path_zc{3}, g_path_hp_tune{1};
+    g_path_zc{3}, g_path_hp_tune{1}, g_path_rec_half{0};
 bool bs_enabled() { return g_path_bs.load(std::memory_order_relaxed) != 0; }
 bool sub_enabled() { return g_path_sub.load(std::memory_order_relaxed) != 0; }
 bool prune_enabled() { return g_path_prune.load(std::memory_order_relaxed) != 0; }
@@ -359,6 +359,7 @@ int rs::unit_width_override() { return g_path_unit_width.load(std::memory_order_
 int rs::hp_tiles_override() { return g_path_hp_tiles.load(std::memory_order_relaxed); }
 int rs::hp_step_override() { return g_path_hp_step.load(std::memory_order_relaxed); }
 bool rs::hp_tune_enabled() { return g_path_hp_tune.load(std::memory_order_relaxed) != 0; }
+bool rs::rec_half_enabled() { return g_path_rec_half.load(std::memory_order_relaxed) != 0; }
 namespace {
 
 // Host half of the encode plan (no device calls): twiddle schedule and panic check.
@@ -2304,6 +2305,14 @@ int rs_debug_split_check(int logm, uint32_t seed) {
     return -1;
 }
 
+int rs_debug_zc_rows(uint8_t *const *rows, int nrows, size_t S) {
+    if (!rows || nrows < 0) return -1;
+    std::vector<int> idx(nrows);
+    for (int i = 0; i < nrows; i++) idx[i] = i;
+    ZcRows z{};
+    return zc_rows(rows, idx, S, z) ? 1 : 0;
+}
+
 int rs_debug_set_path(const char *knob, int value) {
     if (!knob) return RS_ERR_INVALID_ARG;
     const std::string k(knob);
@@ -2314,6 +2323,7 @@ int rs_debug_set_path(const char *knob, int value) {
     else if (k == "hp_tiles" && value >= 0 && value <= 64) g_path_hp_tiles = value;
     else if (k == "hp_step" && value >= 0) g_path_hp_step = value;
     else if (k == "hp_tune" && value >= 0 && value <= 1) g_path_hp_tune = value;
+    else if (k == "rec_half" && value >= 0 && value <= 1) g_path_rec_half = value;
     else if (k == "zc" && value >= 0 && value <= 3) g_path_zc = value;
     else return RS_ERR_INVALID_ARG;
     return RS_OK;

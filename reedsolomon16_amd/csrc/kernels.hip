@@ -1077,12 +1077,19 @@ bool pick_narrow(bool automatic) {
 // SQ_LDS_BANK_CONFLICT -95 %, profiles/r05_sq_counters.txt, r05_lds_pack_ab.txt).  Otherwise the halves keep their global
 // (Leopard 64-byte block) order in rows padded by 16 bytes; the encoder keeps
 // that layout (packed, its 64-byte-tile variant spills).
-template <class F, bool PK = false>
+//
+// PK = 2 (the n >= 1024 reconstruct, round 6): half tiles, 32 bytes of a row
+// per workgroup (two 16-byte units: symbols 16j .. 16j + 15 of a 64-byte
+// block, j = the tile's half), so the n x 32-byte image (64 KB at n = 2048)
+// lets two workgroups share a CU.  The caller addresses a half tile from its
+// block (tile = block * 64) and adds the half's unit offset (2j) to u.
+template <class F, int PK = 0>
 struct LTile {
     static_assert(!F::SYM16 || F::W >= 2, "a GF(2^16) LDS tile must cover whole 64-byte blocks (W >= 2)");
+    static_assert(PK != 2 || (F::SYM16 && F::W == 2), "half tiles: GF(2^16) 16-byte units");
     static constexpr bool W16 = F::SYM16;
-    static constexpr int TB = 32 * F::W;                  // bytes of each row owned by a workgroup
-    static constexpr bool PACK = PK && W16 && F::W == 2;
+    static constexpr int TB = (PK == 2 ? 16 : 32) * F::W;  // bytes of each row owned by a workgroup
+    static constexpr bool PACK = PK != 0 && W16 && F::W == 2;
     static constexpr int ROW = PACK ? TB : TB + 16;  // LDS row stride
     static constexpr int UB = W16 ? 8 * F::W : 4 * F::W;  // global bytes per unit
     static constexpr int U = TB / UB;                     // units per tile
@@ -1135,7 +1142,7 @@ struct LTile {
 // a transform may read its rows from HBM (LdsIn replaced by a loader) and the
 // last may write them out (to HBM, or XOR them into the encoder's
 // accumulator), so the tile is not staged through LDS an extra time.
-template <class F, bool PK = false>
+template <class F, int PK = 0>
 struct LdsIO {
     uint8_t *lds;
     __device__ typename F::Vec operator()(int row, int u) const { return LTile<F, PK>::get(lds, row, u); }
@@ -1143,7 +1150,7 @@ struct LdsIO {
 };
 
 template <class T> struct IsLdsIO : std::false_type {};
-template <class F, bool PK> struct IsLdsIO<LdsIO<F, PK>> : std::true_type {};
+template <class F, int PK> struct IsLdsIO<LdsIO<F, PK>> : std::true_type {};
 
 template <class Fn, int... Is>
 __device__ __forceinline__ void cfor_impl(Fn &&f, std::integer_sequence<int, Is...>) {
@@ -1166,10 +1173,10 @@ __device__ __forceinline__ void lds_sync() { __syncthreads(); }
 // need (forward passes only): skip groups none of whose rows is read later --
 // the pruning of errorBitfield.fftDIT (leopard16.go:1215-1252); the rows that
 // are read come out identical.
-template <class F, bool INV, class In, class Out, class NeedT, int NT = 256>
+template <class F, bool INV, class In, class Out, class NeedT, int NT = 256, int PK = 0>
 __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active, const uint32_t *__restrict__ tw,
                                          NeedT need, const In &in, const Out &out) {
-    typedef LTile<F> L;
+    typedef LTile<F, PK> L;
     typedef typename F::Vec V;
     constexpr int U = L::U;
     if (radix == 4) {
@@ -1239,7 +1246,7 @@ __device__ __forceinline__ void lds_pass(int dist, int radix, int groups_active,
 // as zero, and zero rows transform to zero rows): later passes read those rows.
 // OUT_P1: pass P1 - 1 (the last this call runs) writes through `out` too.
 template <class F, bool INV, int LOGN, class In, class Out, class NeedT = NoNeed, int P0 = 0, int P1 = 32, int NT = 256,
-          bool OUT_P1 = false, bool PK = false>
+          bool OUT_P1 = false, int PK = 0>
 __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const uint32_t *__restrict__ tw,
                                               NeedT need, const In &in, const Out &out) {
     constexpr int N = 1 << LOGN, NP4 = LOGN / 2, NP = NP4 + (LOGN & 1);
@@ -1266,8 +1273,8 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
                 // groups past mtrunc hold zero rows: zero their LDS rows instead
                 // of transforming them (the pass's barrier covers these stores)
                 const int z0 = active * 4 * dist;
-                for (int it = threadIdx.x; it < (N - z0) * LTile<F>::U; it += NT)
-                    lio(z0 + it / LTile<F>::U, it % LTile<F>::U, F::zero());
+                for (int it = threadIdx.x; it < (N - z0) * LTile<F, PK>::U; it += NT)
+                    lio(z0 + it / LTile<F, PK>::U, it % LTile<F, PK>::U, F::zero());
             } else if constexpr (from_hbm) {
                 active = groups;
             }
@@ -1276,8 +1283,8 @@ __device__ __forceinline__ void lds_transform(uint8_t *lds, int mtrunc, const ui
         }
         const uint32_t *t = tw + (uint64_t)slot * F::TWD;
         auto run = [=](const auto &pin, const auto &pout) {
-            if constexpr (INV) lds_pass<F, INV, std::decay_t<decltype(pin)>, std::decay_t<decltype(pout)>, NoNeed, NT>(dist, radix4 ? 4 : 2, active, t, NoNeed{}, pin, pout);
-            else lds_pass<F, INV, std::decay_t<decltype(pin)>, std::decay_t<decltype(pout)>, NeedT, NT>(dist, radix4 ? 4 : 2, active, t, need, pin, pout);
+            if constexpr (INV) lds_pass<F, INV, std::decay_t<decltype(pin)>, std::decay_t<decltype(pout)>, NoNeed, NT, PK>(dist, radix4 ? 4 : 2, active, t, NoNeed{}, pin, pout);
+            else lds_pass<F, INV, std::decay_t<decltype(pin)>, std::decay_t<decltype(pout)>, NeedT, NT, PK>(dist, radix4 ? 4 : 2, active, t, need, pin, pout);
         };
         constexpr bool to_out = p == NP - 1 || (OUT_P1 && p == P1 - 1);
         if constexpr (from_hbm) {
@@ -1309,7 +1316,7 @@ __device__ __forceinline__ void sub_swap(typename F::Vec &v, const uint32_t *__r
 }
 
 // LDS sink that changes rows into subfield coordinates on their way in.
-template <class F, bool PK = false>
+template <class F, int PK = 0>
 struct LdsPsi {
     uint8_t *lds;
     const uint32_t *dmap;
@@ -1328,6 +1335,9 @@ struct LdsPsi {
 // Threads per workgroup: 256, and 1024 for n >= 1024 (the n x 64-byte image
 // leaves room for one or two workgroups per CU: 16 waves keep the SIMDs fed).
 template <int LOGN> constexpr int rec_lds_threads() { return LOGN >= 10 ? 1024 : 256; }
+// PKV = 2 (half tiles, n >= 1024): two 512-thread workgroups per CU, so one
+// workgroup's pass barriers are covered by the other's work.
+template <int LOGN, int PKV> constexpr int rec_threads() { return PKV == 2 ? 512 : rec_lds_threads<LOGN>(); }
 
 // n = 512..2048 with BSUB: the transforms in subfield coordinates wherever
 // every twiddle of a pass lies in GF(2^8) (rec_big_sub_passes; RecArgs::tw_*_sub).
@@ -1336,21 +1346,27 @@ template <int LOGN> struct BigSub {
     static constexpr int FEND = big_sub_fft_end(LOGN);   // FFT passes [0, FEND) subfield
 };
 
-template <class F, class FT, int LOGN, bool BSUB = false>
-__global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) {
-    typedef LTile<F, true> L;  // packed 64-byte tiles (LTile PK)
+template <class F, class FT, int LOGN, bool BSUB = false, int PKV = 1>
+__global__ void __launch_bounds__((rec_threads<LOGN, PKV>()), (PKV == 2 ? 2 : 1)) k_rec_lds(RecArgs a) {
+    typedef LTile<F, PKV> L;  // packed 64-byte tiles (LTile PK), or half tiles (PKV = 2)
     typedef typename F::Vec V;
-    constexpr int N = 1 << LOGN, U = L::U, NT = rec_lds_threads<LOGN>();
+    constexpr int N = 1 << LOGN, U = L::U, NT = rec_threads<LOGN, PKV>();
     constexpr int K = (N * U + NT - 1) / NT;  // derivative outputs per thread
     __shared__ __attribute__((aligned(16))) uint8_t lds[N * L::ROW];
     uint32_t bx = blockIdx.x;
-    if constexpr (LOGN > 8) {
+    if constexpr (PKV == 2) {
+        // half tiles: the four tiles of a 128-byte line go to one XCD: blocks
+        // 32q + x + 8j (j < 4) take tiles 32q + 4x + j
+        if (bx < (gridDim.x & ~31u)) bx = (bx & ~31u) | ((bx & 7u) << 2) | ((bx >> 3) & 3u);
+    } else if constexpr (LOGN > 8) {
         // 64-byte tiles: the two tiles of a 128-byte line go to one XCD
         // (workgroups are dealt round-robin over the 8 XCDs, each with its own
         // L2): blocks 16q + x and 16q + x + 8 take tiles 16q + 2x, 16q + 2x + 1
         if (bx < (gridDim.x & ~15u)) bx = (bx & ~15u) | ((bx & 7u) << 1) | ((bx >> 3) & 1u);
     }
-    const uint64_t tile = (uint64_t)bx * L::TB;
+    // a half tile is addressed from its 64-byte block, its units from uo on
+    const uint64_t tile = PKV == 2 ? (uint64_t)(bx >> 1) * 64 : (uint64_t)bx * L::TB;
+    const int uo = PKV == 2 ? 2 * (int)(bx & 1u) : 0;
     uint8_t *const sbase = a.base ? a.base + (uint64_t)blockIdx.y * a.stripe_stride : nullptr;  // this stripe
     // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0.
     // Branch-free, so the four rows of a first-pass item issue their loads
@@ -1365,10 +1381,11 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
         const RecArgs &a;
         uint64_t tile;
         uint8_t *sbase;
+        int uo;
         __device__ RowLoc locate(int r, int u) const {
             const int i = a.src_idx[r];
             const bool live = i >= 0 && L::valid(tile, a.S, u);
-            return RowLoc{live ? sbase + (uint64_t)i * a.stride + tile : (const uint8_t *)a.tw_in, live ? u : 0, live};
+            return RowLoc{live ? sbase + (uint64_t)i * a.stride + tile : (const uint8_t *)a.tw_in, live ? u + uo : 0, live};
         }
         __device__ RawRow<F> fetch(const RowLoc &l) const { return RawRow<F>{F::load(l.p, l.u), l.live}; }
         __device__ V scale(int r, const RawRow<F> &y) const { return scale_row<F>(y, a.tw_in + (uint64_t)r * F::TWD); }
@@ -1377,10 +1394,11 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
     struct ScaleInTable {
         const RecArgs &a;
         uint64_t tile;
+        int uo;
         __device__ RowLoc locate(int r, int u) const {
             const uint8_t *src = a.src[r];
             const bool live = src && L::valid(tile, a.S, u);
-            return RowLoc{live ? src + tile : (const uint8_t *)a.tw_in, live ? u : 0, live};
+            return RowLoc{live ? src + tile : (const uint8_t *)a.tw_in, live ? u + uo : 0, live};
         }
         __device__ RawRow<F> fetch(const RowLoc &l) const { return RawRow<F>{F::load(l.p, l.u), l.live}; }
         __device__ V scale(int r, const RawRow<F> &y) const { return scale_row<F>(y, a.tw_in + (uint64_t)r * F::TWD); }
@@ -1399,6 +1417,7 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
         uint64_t tile;
         uint8_t *sbase;
         NeedT nw;
+        int uo;
         __device__ void operator()(int r, int u, const V &x) const {
             int j;  // output index of work row r (-1: not revealed)
             if constexpr (BIG) j = a.rev[r];
@@ -1407,32 +1426,32 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
             V v = F::zero();
             F::mul_add(v, x, a.tw_out + (uint64_t)j * F::TWD);
             uint8_t *dst = sbase ? sbase + (uint64_t)a.dst_idx[j] * a.stride : a.dst[j];
-            F::store(dst + tile, u, v);
+            F::store(dst + tile, u + uo, v);
         }
     };
-    const LdsIO<FT, true> lio{lds};
+    const LdsIO<FT, PKV> lio{lds};
     typedef F16S<F::W> FS;  // (BSUB only)
     if constexpr (BSUB) {
         // full-field passes, the last one writing subfield coordinates, then subfield passes
         if (sbase)
-            lds_transform<F, true, LOGN, ScaleInStrided, LdsPsi<F, true>, NoNeed, 0, BigSub<LOGN>::NI, NT, true, true>(
-                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInStrided{a, tile, sbase}, LdsPsi<F, true>{lds, a.tw_dmap});
+            lds_transform<F, true, LOGN, ScaleInStrided, LdsPsi<F, PKV>, NoNeed, 0, BigSub<LOGN>::NI, NT, true, PKV>(
+                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInStrided{a, tile, sbase, uo}, LdsPsi<F, PKV>{lds, a.tw_dmap});
         else
-            lds_transform<F, true, LOGN, ScaleInTable, LdsPsi<F, true>, NoNeed, 0, BigSub<LOGN>::NI, NT, true, true>(
-                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInTable{a, tile}, LdsPsi<F, true>{lds, a.tw_dmap});
-        lds_transform<FS, true, LOGN, LdsIO<FS, true>, LdsIO<FS, true>, NoNeed, BigSub<LOGN>::NI, 32, NT, false, true>(
-            lds, a.mtrunc, a.tw_ifft_sub, NoNeed{}, LdsIO<FS, true>{lds}, LdsIO<FS, true>{lds});
+            lds_transform<F, true, LOGN, ScaleInTable, LdsPsi<F, PKV>, NoNeed, 0, BigSub<LOGN>::NI, NT, true, PKV>(
+                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInTable{a, tile, uo}, LdsPsi<F, PKV>{lds, a.tw_dmap});
+        lds_transform<FS, true, LOGN, LdsIO<FS, PKV>, LdsIO<FS, PKV>, NoNeed, BigSub<LOGN>::NI, 32, NT, false, PKV>(
+            lds, a.mtrunc, a.tw_ifft_sub, NoNeed{}, LdsIO<FS, PKV>{lds}, LdsIO<FS, PKV>{lds});
     } else {
         // the first pass (it reads the rows) per row form, then the rest
         if (sbase)
-            lds_transform<FT, true, LOGN, ScaleInStrided, LdsIO<FT, true>, NoNeed, 0, 1, NT, false, true>(
-                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInStrided{a, tile, sbase}, lio);
+            lds_transform<FT, true, LOGN, ScaleInStrided, LdsIO<FT, PKV>, NoNeed, 0, 1, NT, false, PKV>(
+                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInStrided{a, tile, sbase, uo}, lio);
         else
-            lds_transform<FT, true, LOGN, ScaleInTable, LdsIO<FT, true>, NoNeed, 0, 1, NT, false, true>(
-                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInTable{a, tile}, lio);
-        lds_transform<FT, true, LOGN, LdsIO<FT, true>, LdsIO<FT, true>, NoNeed, 1, 32, NT, false, true>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, lio, lio);
+            lds_transform<FT, true, LOGN, ScaleInTable, LdsIO<FT, PKV>, NoNeed, 0, 1, NT, false, PKV>(
+                lds, a.mtrunc, a.tw_ifft, NoNeed{}, ScaleInTable{a, tile, uo}, lio);
+        lds_transform<FT, true, LOGN, LdsIO<FT, PKV>, LdsIO<FT, PKV>, NoNeed, 1, 32, NT, false, PKV>(lds, a.mtrunc, a.tw_ifft, NoNeed{}, lio, lio);
     }
-    const Reveal rv{a, tile, sbase, need_of()};
+    const Reveal rv{a, tile, sbase, need_of(), uo};
     // formal derivative, closed form: out[r] = in[r] ^ XOR_{b: bit b of r clear} in[r | 2^b]
     if constexpr (LOGN >= 3) {
         // fused with the FFT's first pass (radix-4 at dist D = N/4, one group,
@@ -1476,21 +1495,21 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
         if (a.prune) {
             if constexpr (BSUB) {
                 // subfield passes up to FEND, the last one writing normal coordinates back, then full-field
-                lds_transform<FS, false, LOGN, LdsIO<FS, true>, LdsPsi<F, true>, NeedT, 1, BigSub<LOGN>::FEND, NT, true, true>(
-                    lds, a.mtrunc, a.tw_fft_sub, need_of(), LdsIO<FS, true>{lds}, LdsPsi<F, true>{lds, a.tw_dmap});
-                lds_transform<F, false, LOGN, LdsIO<F, true>, Reveal, NeedT, BigSub<LOGN>::FEND, 32, NT, false, true>(
-                    lds, a.mtrunc, a.tw_fft, need_of(), LdsIO<F, true>{lds}, rv);
+                lds_transform<FS, false, LOGN, LdsIO<FS, PKV>, LdsPsi<F, PKV>, NeedT, 1, BigSub<LOGN>::FEND, NT, true, PKV>(
+                    lds, a.mtrunc, a.tw_fft_sub, need_of(), LdsIO<FS, PKV>{lds}, LdsPsi<F, PKV>{lds, a.tw_dmap});
+                lds_transform<F, false, LOGN, LdsIO<F, PKV>, Reveal, NeedT, BigSub<LOGN>::FEND, 32, NT, false, PKV>(
+                    lds, a.mtrunc, a.tw_fft, need_of(), LdsIO<F, PKV>{lds}, rv);
             } else {
-                lds_transform<FT, false, LOGN, LdsIO<FT, true>, Reveal, NeedT, 1, 32, NT, false, true>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
+                lds_transform<FT, false, LOGN, LdsIO<FT, PKV>, Reveal, NeedT, 1, 32, NT, false, PKV>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
             }
         } else {
             if constexpr (BSUB) {
-                lds_transform<FS, false, LOGN, LdsIO<FS, true>, LdsPsi<F, true>, NoNeed, 1, BigSub<LOGN>::FEND, NT, true, true>(
-                    lds, a.mtrunc, a.tw_fft_sub, NoNeed{}, LdsIO<FS, true>{lds}, LdsPsi<F, true>{lds, a.tw_dmap});
-                lds_transform<F, false, LOGN, LdsIO<F, true>, Reveal, NoNeed, BigSub<LOGN>::FEND, 32, NT, false, true>(
-                    lds, a.mtrunc, a.tw_fft, NoNeed{}, LdsIO<F, true>{lds}, rv);
+                lds_transform<FS, false, LOGN, LdsIO<FS, PKV>, LdsPsi<F, PKV>, NoNeed, 1, BigSub<LOGN>::FEND, NT, true, PKV>(
+                    lds, a.mtrunc, a.tw_fft_sub, NoNeed{}, LdsIO<FS, PKV>{lds}, LdsPsi<F, PKV>{lds, a.tw_dmap});
+                lds_transform<F, false, LOGN, LdsIO<F, PKV>, Reveal, NoNeed, BigSub<LOGN>::FEND, 32, NT, false, PKV>(
+                    lds, a.mtrunc, a.tw_fft, NoNeed{}, LdsIO<F, PKV>{lds}, rv);
             } else {
-                lds_transform<FT, false, LOGN, LdsIO<FT, true>, Reveal, NoNeed, 1, 32, NT, false, true>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
+                lds_transform<FT, false, LOGN, LdsIO<FT, PKV>, Reveal, NoNeed, 1, 32, NT, false, PKV>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
             }
         }
         return;
@@ -1519,9 +1538,9 @@ __global__ void __launch_bounds__(rec_lds_threads<LOGN>()) k_rec_lds(RecArgs a) 
         __syncthreads();
     }
     if (a.prune) {
-        lds_transform<FT, false, LOGN, LdsIO<FT, true>, Reveal, NeedT, 0, 32, NT, false, true>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
+        lds_transform<FT, false, LOGN, LdsIO<FT, PKV>, Reveal, NeedT, 0, 32, NT, false, PKV>(lds, a.mtrunc, a.tw_fft, need_of(), lio, rv);
     } else {
-        lds_transform<FT, false, LOGN, LdsIO<FT, true>, Reveal, NoNeed, 0, 32, NT, false, true>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
+        lds_transform<FT, false, LOGN, LdsIO<FT, PKV>, Reveal, NoNeed, 0, 32, NT, false, PKV>(lds, a.mtrunc, a.tw_fft, NoNeed{}, lio, rv);
     }
 }
 
@@ -1663,21 +1682,29 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
     }
 }
 
-template <class F, class FT, int LOGN, bool BSUB>
+template <class F, class FT, int LOGN, bool BSUB, int PKV = 1>
 hipError_t rec_lds_tb(const RecArgs &a, hipStream_t s) {
-    const unsigned gx = (unsigned)((a.S + LTile<F>::TB - 1) / LTile<F>::TB);
+    constexpr int TB = LTile<F, PKV>::TB, NT = rec_threads<LOGN, PKV>();
+    const unsigned gx = (unsigned)((a.S + TB - 1) / TB);
     if (!a.base || a.nstripes <= 1) {
-        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN, BSUB>), dim3(gx), dim3(rec_lds_threads<LOGN>()), 0, s, a);
+        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN, BSUB, PKV>), dim3(gx), dim3(NT), 0, s, a);
         return hipGetLastError();
     }
     return for_y(a.nstripes, [&](int y0, int ny) {  // batched strided stripes: grid.y = stripe
         RecArgs b = a;
         b.base = a.base + (uint64_t)y0 * a.stripe_stride;
-        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN, BSUB>), dim3(gx, (unsigned)ny), dim3(rec_lds_threads<LOGN>()), 0, s, b);
+        hipLaunchKernelGGL((k_rec_lds<F, FT, LOGN, BSUB, PKV>), dim3(gx, (unsigned)ny), dim3(NT), 0, s, b);
     });
 }
 template <class F, class FT, int LOGN>
 hipError_t rec_lds_t(const RecArgs &a, hipStream_t s) {
+    if constexpr (LOGN >= 10 && std::is_same<F, F16<2>>::value) {
+        // n = 1024, 2048: half tiles, two workgroups per CU (rs_debug_set_path "rec_half")
+        if (rec_half_enabled()) {
+            if (a.tw_ifft_sub && a.tw_fft_sub && a.tw_dmap) return rec_lds_tb<F, FT, LOGN, true, 2>(a, s);
+            return rec_lds_tb<F, FT, LOGN, false, 2>(a, s);
+        }
+    }
     if constexpr (LOGN > 8)
         if (a.tw_ifft_sub && a.tw_fft_sub && a.tw_dmap) return rec_lds_tb<F, FT, LOGN, true>(a, s);
     return rec_lds_tb<F, FT, LOGN, false>(a, s);

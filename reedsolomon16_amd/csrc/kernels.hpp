@@ -64,6 +64,7 @@ int unit_width_override();
 int hp_tiles_override();
 int hp_step_override();
 bool hp_tune_enabled();
+bool rec_half_enabled();
 
 hipError_t launch_encode_reg(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 // Half-wave split encode (GF(2^16), logm 2..5, strided rows only: data.table ==

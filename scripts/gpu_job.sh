@@ -18,6 +18,7 @@
 #   sweep=ARGS           python scripts/c3_tpw_sweep.py ARGS (comma-less args split on ':')
 #   probe                scripts/micro/launch_probe (C driver: host vs GPU time per call)
 #   py=SCRIPT[@ARGS]     python SCRIPT ARGS (ARGS split on ':')
+#   pmcpy=COUNTERS@SCRIPT[@ARGS]  one rocprofv3 --pmc pass over python3 SCRIPT ARGS
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=$1
@@ -55,6 +56,13 @@ for step in "$@"; do
       run 300 "$n-pmc" rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "$OUT/pmc$n" -o run -- python3 bench.py $QUIET --steps 50 --warmup 5 ${args//,/ } ;;
     sweep) run 600 "$n-sweep" python3 scripts/c3_tpw_sweep.py ${val//:/ } ;;
     probe) run 120 "$n-probe" scripts/micro/launch_probe ;;
+    pmcpy)
+      ctr=${val%%@*}
+      rest=${val#*@}
+      scr=${rest%%@*}
+      args=""
+      [ "$rest" != "$scr" ] && args=${rest#*@}
+      run 300 "$n-pmcpy" rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "$OUT/pmc$n" -o run -- python3 "$scr" ${args//:/ } ;;
     py)
       scr=${val%%@*}
       args=""

@@ -151,11 +151,17 @@ def main():
     ap.add_argument("--configs", default="C3")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--knobs", default="", help="rs_debug_set_path knobs, e.g. rec_half=1,hp_tiles=4")
     a = ap.parse_args()
     import numpy as np
     import torch
 
     import reedsolomon16_amd as rs
+    from reedsolomon16_amd import _capi
+
+    for kv in filter(None, a.knobs.split(",")):
+        kn, val = kv.split("=")
+        _capi.set_path(kn, int(val))
 
     for name in a.configs.split(","):
         if name in HOST_CONFIGS:
@@ -197,7 +203,7 @@ def main():
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.iters
         alg = ns * (k + p) * S
-        print(json.dumps({"tag": a.tag, "config": name, "op": op, "path": c.encode_path, "erased": int(ne) if op == "reconstruct" else 0,
+        print(json.dumps({"tag": a.tag, "knobs": a.knobs, "config": name, "op": op, "path": c.encode_path, "erased": int(ne) if op == "reconstruct" else 0,
                           "prune": os.environ.get("RS_NO_PRUNE", "0") != "1", "us": round(us, 2),
                           "GBps_alg": round(alg / us / 1e3, 1), "frac": round(alg / us / 1e3 / 8000, 4)}), flush=True)
 

@@ -572,6 +572,43 @@ def test_host_reconstruct_zero_copy(paths, zc, bits, k, p, S, rows):
         assert c._L.rs_host_unregister(reg.ctypes.data) == 0
 
 
+def test_zero_copy_rows_checked_at_both_ends():
+    """A row that starts in registered (mapped) host memory and runs past the
+    registered range (advisor finding, round 5) must not go to the zero-copy
+    kernels, which would read or write unmapped addresses: the codec checks
+    both ends of every row (codec.cpp zc_rows, probed through
+    rs_debug_zc_rows: pointer queries only, nothing touches the short row)."""
+    import ctypes as C
+
+    L = rs.lib()
+    S, n = 1 << 16, 4
+    raw = np.zeros(n * S + 8192, np.uint8)
+    o = (-raw.ctypes.data) % 4096
+    slab = raw[o:o + n * S]
+    rows = (C.c_void_p * n)(*[slab.ctypes.data + i * S for i in range(n)])
+    assert L.rs_debug_zc_rows(rows, n, S) == 0  # pageable
+    assert L.rs_host_register(slab.ctypes.data, n * S) == 0
+    try:
+        assert L.rs_debug_zc_rows(rows, n, S) == 1  # every row mapped end to end
+    finally:
+        assert L.rs_host_unregister(slab.ctypes.data) == 0
+    # registered up to the middle of the last row (a page-aligned cut)
+    assert L.rs_host_register(slab.ctypes.data, (n - 1) * S + S // 2) == 0
+    try:
+        assert L.rs_debug_zc_rows(rows, n - 1, S) == 1
+        assert L.rs_debug_zc_rows(rows, n, S) == 0
+        one = (C.c_void_p * 1)(slab.ctypes.data + (n - 1) * S)
+        assert L.rs_debug_zc_rows(one, 1, S // 2) == 1 and L.rs_debug_zc_rows(one, 1, S) == 0
+    finally:
+        assert L.rs_host_unregister(slab.ctypes.data) == 0
+    # two separate pinned blocks: a "row" reaching from one into the next is refused
+    a, b = rs.alloc_pinned(S), rs.alloc_pinned(S)
+    r = (C.c_void_p * 1)(a.ctypes.data + S // 2)
+    assert L.rs_debug_zc_rows(r, 1, S // 2) == 1
+    if b.ctypes.data != a.ctypes.data + S:  # (adjacent only by chance)
+        assert L.rs_debug_zc_rows(r, 1, S) == 0
+
+
 # Batched device reconstruct (rs_reconstruct_dev_batch): one erasure pattern
 # over many stripes in one launch, rows at a padded stride and stripes at a
 # padded stripe stride; n <= 256 codecs run the LDS kernel with grid.y =

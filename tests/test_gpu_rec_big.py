@@ -22,6 +22,15 @@ def torch():
     return t
 
 
+@pytest.fixture(params=[0, 1], ids=["tiles64", "half32"], autouse=True)
+def tile_mode(request, paths):
+    """Every test twice: 64-byte tiles, one workgroup per CU, and (round 6)
+    32-byte half tiles, two workgroups per CU (rs_debug_set_path rec_half;
+    n = 1024 and 2048 only)."""
+    paths("rec_half", request.param)
+    return request.param
+
+
 def patterns(k, p, seed):
     rng = np.random.default_rng(seed)
     return {
