@@ -264,3 +264,29 @@ def test_multi_parts_device_resident():
     torch.cuda.synchronize()
     assert torch.equal(slab, ref)
     c.close()
+
+
+@pytest.mark.parametrize("bits", [16, 8])
+def test_multi_stream_methods_match_single_codec(bits):
+    """The interface's Stream* methods (rsStream16 / rsStreamFF8 loops over the
+    async tickets, stream.py) on a multi-device codec: every 4 MiB block is
+    split over the parts, and the writers get the same bytes as on one device."""
+    import io
+
+    k, p, n = 10, 4, (4 << 20) + 4160  # a full block, then a short one (64-byte multiple: no GF(2^16) verify panic)
+    rng = np.random.default_rng(bits)
+    data = rng.integers(0, 256, (k, n), dtype=np.uint8)
+    outs = []
+    for devs in (None, DEV4):
+        c = rs.ReedSolomon(k, p, bits, devices=devs)
+        par = [io.BytesIO() for _ in range(p)]
+        c.stream_encode([io.BytesIO(data[i].tobytes()) for i in range(k)], par)
+        pv = [x.getvalue() for x in par]
+        ok = c.stream_verify([io.BytesIO(data[i].tobytes()) for i in range(k)] + [io.BytesIO(v) for v in pv])
+        ins = [None if i in (1, 4) else io.BytesIO(data[i].tobytes()) for i in range(k)] + [io.BytesIO(v) for v in pv]
+        rec = [io.BytesIO() if i in (1, 4) else None for i in range(k + p)]
+        c.stream_reconstruct(ins, rec)
+        outs.append((pv, ok, [r.getvalue() for r in rec if r is not None]))
+        c.close()
+    assert outs[0] == outs[1]
+    assert outs[0][2] == [data[1].tobytes(), data[4].tobytes()]
