@@ -684,14 +684,22 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
                 // the phase-2 / phase-3 waves sharing its SIMD (C4 x 16 1692 ->
                 // 1637 us, one stripe 124 -> 121 us; raising the phase-3 waves too
                 // gained nothing, profiles/r03_c4_prio_ab.txt).
+                const int lab = d.args().lab;
                 if (slot == 0) __builtin_amdgcn_s_setprio(3);
+                else if (lab & 4) __builtin_amdgcn_s_setprio(1);
                 set_tile(tn);
                 const int n1 = slot == 0 && p1b >= 0 ? 2 : 1;
                 // (loading unit b's rows into V[8..15] up front measured slower:
                 // 1950 vs 1694 us per 16 C4 stripes)
 #pragma nounroll
                 for (int s = 0; s < n1; s++) {
-                    if (s) d.park_swap();
+                    if (s) {
+                        d.park_swap();
+                        // lab: an early wave's second unit is off the critical path
+                        // (the early waves wait at the image-free barrier): drop its priority
+                        if (lab & 1) __builtin_amdgcn_s_setprio(0);
+                        else if (lab & 2) __builtin_amdgcn_s_setprio(1);
+                    }
                     d.phase1(s ? p1b : p1a, slot == 0 && s == 0 && cur ? 2 : 0);
                 }
                 __builtin_amdgcn_s_setprio(0);

@@ -349,7 +349,7 @@ int upload_split(rs_codec *c) {
 // the reconstruct FFT unpruned, the narrow / wide LDS units) on the same small
 // inputs.  Process-wide; read when a codec is created (bs) or at each launch.
 std::atomic<int> g_path_bs{1}, g_path_sub{1}, g_path_prune{1}, g_path_unit_width{-1}, g_path_hp_tiles{0}, g_path_hp_step{0},
-    g_path_zc{3}, g_path_hp_tune{1}, g_path_rec_half{0};
+    g_path_zc{3}, g_path_hp_tune{1}, g_path_rec_half{0}, g_path_dec_lab{0};
 bool bs_enabled() { return g_path_bs.load(std::memory_order_relaxed) != 0; }
 bool sub_enabled() { return g_path_sub.load(std::memory_order_relaxed) != 0; }
 bool prune_enabled() { return g_path_prune.load(std::memory_order_relaxed) != 0; }
@@ -909,6 +909,7 @@ int launch_reconstruct(rs_codec *c, const RecPlan &pl, int set, uint64_t S, hipS
         ra.m = c->m;
         ra.nd = nd;
         ra.prune = prune_enabled() ? 1 : 0;
+    ra.lab = g_path_dec_lab.load(std::memory_order_relaxed);
         for (int p : pl.pos) ra.need[p >> 5] |= 1u << (p & 31);
         HIP_TRY(launch_rec_lds(c->bits, c->logn, c->dec_sub, ra, s));
         return RS_OK;
@@ -1005,6 +1006,7 @@ int launch_rec_plan(rs_codec *c, DevPlan *dpl, uint8_t *base, uint64_t stride, u
     ra.m = c->m;
     ra.nd = nd;
     ra.prune = prune_enabled() ? 1 : 0;
+    ra.lab = g_path_dec_lab.load(std::memory_order_relaxed);
     std::memcpy(ra.need, dpl->need, sizeof(ra.need));
     ra.need_w = dpl->need_w;
     ra.rev = dpl->rev;
@@ -1043,6 +1045,7 @@ int reconstruct_device_lds(rs_codec *c, uint8_t *const *d, const std::vector<uin
     ra.m = c->m;
     ra.nd = nd;
     ra.prune = prune_enabled() ? 1 : 0;
+    ra.lab = g_path_dec_lab.load(std::memory_order_relaxed);
     std::memcpy(ra.need, dp->need, sizeof(ra.need));
     ra.need_w = dp->need_w;
     ra.rev = dp->rev;
@@ -2324,6 +2327,7 @@ int rs_debug_set_path(const char *knob, int value) {
     else if (k == "hp_step" && value >= 0) g_path_hp_step = value;
     else if (k == "hp_tune" && value >= 0 && value <= 1) g_path_hp_tune = value;
     else if (k == "rec_half" && value >= 0 && value <= 1) g_path_rec_half = value;
+    else if (k == "dec_lab" && value >= 0 && value <= 255) g_path_dec_lab = value;
     else if (k == "zc" && value >= 0 && value <= 3) g_path_zc = value;
     else return RS_ERR_INVALID_ARG;
     return RS_OK;

@@ -146,6 +146,9 @@ struct RecArgs {
     // is full-field) of the passes kernels.hip BigSub<logn> runs in subfield
     // coordinates, and the coordinate-change map; nullptr: full field throughout
     const uint32_t *tw_ifft_sub, *tw_fft_sub, *tw_dmap;
+    // schedule variants of the bit-sliced n = 256 decoder (rs_debug_set_path
+    // "dec_lab"; 0 = the product schedule; lab A/B only)
+    int lab;
 };
 // sub: GF(2^16) transforms in subfield coordinates (tw_ifft/tw_fft are
 // kTwDwords8 subfield tables; tw_in/tw_out fold in the coordinate change).

@@ -101,9 +101,14 @@ struct Multi {
 Multi *multi_create(std::vector<rs_codec *> parts, std::vector<int> devices) {
     Multi *m = new (std::nothrow) Multi();
     if (!m) return nullptr;
+    try {  // thread creation can fail: no exception crosses the C-ABI
+        for (size_t g = 0; g < parts.size(); g++) m->workers.emplace_back(new Worker());
+    } catch (...) {
+        delete m;  // joins the workers already started; the caller still owns the parts
+        return nullptr;
+    }
     m->parts = std::move(parts);
     m->devices = std::move(devices);
-    for (size_t g = 0; g < m->parts.size(); g++) m->workers.emplace_back(new Worker());
     return m;
 }
 
