@@ -194,6 +194,8 @@ struct Dec {
     // ---------------- phase 1: rows 16 u .. 16 u + 15 into V[0..7]
     // all 16 row loads in flight at once, straight into the row registers
     // (missing rows read as zero through an empty range)
+    // (RO = 8: into V[8..15], the registers phase 3 leaves alone)
+    template <int RO = 0>
     __device__ __forceinline__ void load_rows(int u) {
         cargs_t &a = args();
         const uint32_t off = lane_off();
@@ -201,7 +203,7 @@ struct Dec {
             constexpr int t = decltype(T)::value;
             const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(src_rsrc(a, 16 * u + t), off, 0, 0);
 #pragma unroll
-            for (int d = 0; d < 4; d++) V[t >> 1][4 * (t & 1) + d] = x[d];
+            for (int d = 0; d < 4; d++) V[RO + (t >> 1)][4 * (t & 1) + d] = x[d];
         });
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -362,7 +364,8 @@ struct Dec {
     // phase 2's two barriers there, so it does not hold phase 2 back; after the
     // scaling / after the transpose measured 1753 / 1704 against 1690 us per
     // 16 C4 stripes, profiles/r03_c4_bsdec_units_ab.txt)
-    __device__ __forceinline__ void phase1(int u, int nbar = 0) {
+    // pre: the unit's rows are already loaded into V[0..7] (load_rows issued earlier)
+    __device__ __forceinline__ void phase1(int u, int nbar = 0, bool pre = false) {
         if (16 * u >= args().mtrunc) {  // rows past mtrunc: zero (the image rows still have to be written)
 #pragma unroll
             for (int i = 0; i < 8; i++)
@@ -371,7 +374,14 @@ struct Dec {
             for (int b = 0; b < nbar; b++) lds_barrier();
             return;
         }
-        load_rows(u);
+        if (pre) {  // rows preloaded into V[8..15] (late waves, lab bit 8)
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) V[i][k] = V[8 + i][k];
+        } else {
+            load_rows(u);
+        }
         scale(u);
         ifft0_bytes(u);
         for (int b = 0; b < nbar; b++) lds_barrier();
@@ -635,6 +645,7 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
         // The last iteration has no phase 1: waves 8.. take the second phase-3
         // units of waves 0.. (so every phase-3 unit runs on a wave of its own).
         int p3a = u3a, p3b = u3b;
+        bool pre = false;  // a late wave's phase-1 rows already in flight (lab bit 8)
         if (!more) {
             if (early) {
                 p3a = (int)((uint32_t)(pl.code[0] >> (16 * (w - 8))) >> 4 & 15u) - 1;
@@ -661,6 +672,13 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
                     asm volatile("" : "+s"(wt));
 #pragma unroll
                     for (int q = 0; q < Dec<STRIDED>::NQ; q++) d.img_put(2 * wt + 16 * q, d.V[q]);
+                    // lab bit 8: a late wave with no phase-3 unit issues its phase-1
+                    // unit's row loads now, so they are in flight across the Y barrier
+                    if ((d.args().lab & 8) && more && p1a >= 0 && p3a < 0 && 16 * p1a < d.args().mtrunc) {
+                        set_tile(tn);
+                        d.template load_rows<8>(p1a);
+                        pre = true;
+                    }
                 }
                 if (!early_p1) lds_barrier();  // Y is in the image
                 if (p3a >= 0) {
@@ -700,7 +718,7 @@ __global__ void __launch_bounds__(64 * kWaves, kWaves / 4) k_rec_bs256(RecArgs a
                         if (lab & 1) __builtin_amdgcn_s_setprio(0);
                         else if (lab & 2) __builtin_amdgcn_s_setprio(1);
                     }
-                    d.phase1(s ? p1b : p1a, slot == 0 && s == 0 && cur ? 2 : 0);
+                    d.phase1(s ? p1b : p1a, slot == 0 && s == 0 && cur ? 2 : 0, slot == 1 && pre);
                 }
                 __builtin_amdgcn_s_setprio(0);
             }

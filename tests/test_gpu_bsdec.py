@@ -20,6 +20,15 @@ GEOMS = [(128, 32, 4096), (128, 32, 1088), (96, 64, 2048), (120, 20, 1024 + 192)
          (30, 100, 1024), (1, 128, 2048), (144, 9, 512)]
 
 
+@pytest.fixture(params=[0, 8], ids=["product", "preload"], autouse=True)
+def schedule(request, paths):
+    """Every test under the product schedule and (round 6, rs_debug_set_path
+    dec_lab bit 8) with the late phase-1 waves' row loads issued before the
+    Y barrier, into V[8..15]."""
+    paths("dec_lab", request.param)
+    return request.param
+
+
 def patterns(rng, k, p):
     n = k + p
     pats = [list(range(min(p, k))), list(range(k, k + p)), [0], [n - 1], [k - 1, k],
