@@ -448,9 +448,18 @@ class HpTuner {
             std::sort(x, x + kTrials / 2 - 1);
             return x[(kTrials / 2 - 1) / 2];
         };
-        t.pick = ok && med(ms[1]) < med(ms[0]) ? 1 : kMany;
-        if (m_.size() > 256) m_.clear();  // shapes of a long-lived process: re-tune rather than grow
-        return t.pick;
+        const int pick = ok && med(ms[1]) < med(ms[0]) ? 1 : kMany;
+        t.pick = pick;
+        if (m_.size() > 256) {  // shapes of a long-lived process: re-tune rather than grow
+            for (auto &kv : m_)
+                if (!kv.second.pick)
+                    for (int i = 0; i < kv.second.n; i++) {  // (a pending event is released once it completes)
+                        (void)hipEventDestroy(kv.second.ev[i][0]);
+                        (void)hipEventDestroy(kv.second.ev[i][1]);
+                    }
+            m_.clear();
+        }
+        return pick;
     }
     static constexpr int kMany = 4;
 
