@@ -83,7 +83,7 @@ def lib() -> C.CDLL:
     return L
 
 
-_PATH_DEFAULTS = {"bs": 1, "sub": 1, "prune": 1, "unit_width": -1, "hp_tiles": 0, "hp_step": 0, "zc": 3, "hp_tune": 1, "rec_half": 0, "dec_lab": 0}
+_PATH_DEFAULTS = {"bs": 1, "sub": 1, "prune": 1, "unit_width": -1, "hp_tiles": 0, "hp_step": 0, "zc": 3, "hp_tune": 1, "rec_half": 0, "dec_lab": 0, "lds_big": 1}
 
 
 def set_path(knob: str, value: int) -> None:

@@ -349,7 +349,7 @@ int upload_split(rs_codec *c) {
 // the reconstruct FFT unpruned, the narrow / wide LDS units) on the same small
 // inputs.  Process-wide; read when a codec is created (bs) or at each launch.
 std::atomic<int> g_path_bs{1}, g_path_sub{1}, g_path_prune{1}, g_path_unit_width{-1}, g_path_hp_tiles{0}, g_path_hp_step{0},
-    g_path_zc{3}, g_path_hp_tune{1}, g_path_rec_half{0}, g_path_dec_lab{0};
+    g_path_zc{3}, g_path_hp_tune{1}, g_path_rec_half{0}, g_path_dec_lab{0}, g_path_lds_big{1};
 bool bs_enabled() { return g_path_bs.load(std::memory_order_relaxed) != 0; }
 bool sub_enabled() { return g_path_sub.load(std::memory_order_relaxed) != 0; }
 bool prune_enabled() { return g_path_prune.load(std::memory_order_relaxed) != 0; }
@@ -362,11 +362,19 @@ bool rs::hp_tune_enabled() { return g_path_hp_tune.load(std::memory_order_relaxe
 bool rs::rec_half_enabled() { return g_path_rec_half.load(std::memory_order_relaxed) != 0; }
 namespace {
 
+// One LDS-resident encode launch covers m <= 256 (both fields) and, for
+// GF(2^16), m up to 1024 (64-byte tiles, kernels.hpp kMaxLdsEncLogM16);
+// larger m runs the multi-pass kernels.
+bool enc_lds_ok(const rs_codec *c) {
+    return c->logm <= kMaxLdsLogN ||
+           (c->bits == 16 && c->logm <= kMaxLdsEncLogM16 && g_path_lds_big.load(std::memory_order_relaxed));
+}
+
 // Host half of the encode plan (no device calls): twiddle schedule and panic check.
 void plan_encode_host(rs_codec *c) {
     c->enc_ok = encode_schedule(*c->F, c->k, c->p, c->enc_ifft_logs, c->enc_fft_logs, c->nchunks);
     c->path = !c->enc_ok ? "panic" : (c->logm <= kMaxRegLogM ? encode_reg_name(c->bits, c->logm)
-                                                   : c->logm <= kMaxLdsLogN ? "lds-m" + std::to_string(c->m) : "multipass");
+                                                   : enc_lds_ok(c) ? "lds-m" + std::to_string(c->m) : "multipass");
     if (c->enc_ok && c->bits == 16 && c->logm >= 2 && c->logm <= 5)
         c->path = std::string("split16-m") + std::to_string(c->m);
     c->bs_ok = c->enc_ok && c->bits == 16 && (c->logm == 4 || c->logm == 5) && bs_enabled() &&
@@ -542,7 +550,7 @@ int scratch_host_wait(rs_codec *c) {
 // scratch event: one hipEventRecord less per call (the single-stripe
 // device-resident encode is host-bound).
 bool encode_uses_scratch(const rs_codec *c, const RowSet &data, const RowSet &par) {
-    return data.table || par.table || c->logm > kMaxLdsLogN;
+    return data.table || par.table || !enc_lds_ok(c);
 }
 // Mark the scratch as used by the work queued on `s` so far.
 int scratch_release(rs_codec *c, hipStream_t s) {
@@ -671,7 +679,7 @@ int encode_device(rs_codec *c, RowSet data, RowSet par, uint64_t S, uint64_t str
         HIP_TRY(launch_encode_reg(c->bits, c->logm, mismatch != nullptr, a, s));
         return RS_OK;
     }
-    if (c->logm <= kMaxLdsLogN) {  // m rows of accumulator + chunk LDS-resident
+    if (enc_lds_ok(c)) {  // m rows of accumulator + chunk LDS-resident
         EncodeArgs a{};
         a.data = data;
         a.parity = par;
@@ -1356,7 +1364,7 @@ int host_pipeline(rs_codec *c, uint8_t *const *shards, uint64_t S, HostOp op, co
     // scratch of the multi-pass paths, sized before any launch (no realloc mid-pipeline)
     // (the LDS-resident reconstruct plan and the m <= 256 LDS encode use none)
     if (op == HostOp::Reconstruct && !dpl) e = scratch_ensure(c, c->work, (size_t)c->n * seg);
-    else if (op != HostOp::Reconstruct && c->logm > kMaxLdsLogN) e = scratch_ensure(c, c->work, (size_t)2 * c->m * seg);
+    else if (op != HostOp::Reconstruct && !enc_lds_ok(c)) e = scratch_ensure(c, c->work, (size_t)2 * c->m * seg);
     if (e) return e;
     // outputs in pageable memory go D2H into a pinned bounce slab, and the host
     // copies segment j - 1 out while the device works on segment j
@@ -2328,6 +2336,7 @@ int rs_debug_set_path(const char *knob, int value) {
     else if (k == "hp_tune" && value >= 0 && value <= 1) g_path_hp_tune = value;
     else if (k == "rec_half" && value >= 0 && value <= 1) g_path_rec_half = value;
     else if (k == "dec_lab" && value >= 0 && value <= 255) g_path_dec_lab = value;
+    else if (k == "lds_big" && value >= 0 && value <= 1) g_path_lds_big = value;
     else if (k == "zc" && value >= 0 && value <= 3) g_path_zc = value;
     else return RS_ERR_INVALID_ARG;
     return RS_OK;

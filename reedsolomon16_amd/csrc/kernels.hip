@@ -1551,11 +1551,15 @@ __global__ void __launch_bounds__((rec_threads<LOGN, PKV>()), (PKV == 2 ? 2 : 1)
 // rows (or compares them, verify).
 // FT: the field of the final FFT (F16S: subfield coordinates, EncodeArgs::tw_fft_sub).
 // ISUB: the chunk IFFTs' subfield passes (EncodeArgs::tw_ifft_sub; needs FT = F16S).
+// m = 512, 1024 (GF(2^16), round 6): 64-byte tiles (F16<2>) and one
+// 1024-thread workgroup per CU, the m x 80-byte image(s) taking 80 KB of LDS
+// (m = 1024: acc in registers, one image; m = 512: acc and chunk images).
+template <int LOGM> constexpr int enc_threads() { return LOGM >= 9 ? 1024 : 256; }
 template <class F, int LOGM, bool VERIFY, class FT = F, bool ISUB = false>
-__global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
+__global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_enc_lds(EncodeArgs a) {
     typedef LTile<F> L;
     typedef typename F::Vec V;
-    constexpr int M = 1 << LOGM;
+    constexpr int M = 1 << LOGM, NT = enc_threads<LOGM>();
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
     constexpr bool ACCR = enc_acc_regs(LOGM);
     uint8_t *acc = lds_dyn, *cur = ACCR ? lds_dyn : lds_dyn + M * L::ROW;
@@ -1599,7 +1603,7 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
         // mapping, so a thread keeps acc rows i + qD of its items across the
         // chunks and the LDS holds only the current chunk.
         constexpr int NP = LOGM / 2, D = M / 4;
-        constexpr int KF = (D * L::U + 255) / 256;  // items per thread
+        constexpr int KF = (D * L::U + NT - 1) / NT;  // items per thread
         constexpr int last = [] {  // twiddle slot of the IFFT's last pass
             int sl = 0;
             for (int q = 0; q < NP - 1; q++) sl += 3 * (M / (4 << (2 * q)));
@@ -1620,17 +1624,17 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
                 const LdsPsi<F> psi{cur, a.tw_dmap};
                 const LdsIO<FT> lios{cur};
                 const int nff = a.ifft_nff[c];  // 1 or 2 (codec.cpp upload_ifft_sub)
-                if (nff == 1) lds_transform<F, true, LOGM, ChunkIn, LdsPsi<F>, NoNeed, 0, 1, 256, true>(cur, cnt, tw, NoNeed{}, in, psi);
-                else lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, 1>(cur, cnt, tw, NoNeed{}, in, lio);
-                if (nff == 2) lds_transform<F, true, LOGM, LdsIO<F>, LdsPsi<F>, NoNeed, 1, 2, 256, true>(cur, cnt, tw, NoNeed{}, lio, psi);
-                else lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 1, 2>(cur, cnt, tws, NoNeed{}, lios, lios);
-                lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 2, NP - 1>(cur, cnt, tws, NoNeed{}, lios, lios);
+                if (nff == 1) lds_transform<F, true, LOGM, ChunkIn, LdsPsi<F>, NoNeed, 0, 1, NT, true>(cur, cnt, tw, NoNeed{}, in, psi);
+                else lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, 1, NT>(cur, cnt, tw, NoNeed{}, in, lio);
+                if (nff == 2) lds_transform<F, true, LOGM, LdsIO<F>, LdsPsi<F>, NoNeed, 1, 2, NT, true>(cur, cnt, tw, NoNeed{}, lio, psi);
+                else lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 1, 2, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
+                lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 2, NP - 1, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
             } else {
-                lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, NP - 1>(cur, cnt, tw, NoNeed{}, in, lio);
+                lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, NP - 1, NT>(cur, cnt, tw, NoNeed{}, in, lio);
             }
 #pragma unroll
             for (int k = 0; k < KF; k++) {
-                const int it = threadIdx.x + 256 * k;
+                const int it = threadIdx.x + NT * k;
                 if (it < D * L::U) {
                     const int i = it / L::U, u = it - i * L::U;
                     V x[4];
@@ -1651,7 +1655,7 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
         const uint32_t *twf = SUB ? a.tw_fft_sub : a.tw_fft;
 #pragma unroll
         for (int k = 0; k < KF; k++) {
-            const int it = threadIdx.x + 256 * k;
+            const int it = threadIdx.x + NT * k;
             if (it < D * L::U) {
                 const int i = it / L::U, u = it - i * L::U;
                 if constexpr (SUB && !isub)  // (a subfield IFFT leaves acc in subfield coordinates already)
@@ -1663,7 +1667,7 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
             }
         }
         __syncthreads();
-        lds_transform<FT, false, LOGM, LdsIO<FT>, ParityOut, NoNeed, 1>(cur, a.p, twf, NoNeed{}, LdsIO<FT>{cur},
+        lds_transform<FT, false, LOGM, LdsIO<FT>, ParityOut, NoNeed, 1, 32, NT>(cur, a.p, twf, NoNeed{}, LdsIO<FT>{cur},
                                                                          ParityOut{a, soff, tile, &bad});
         if constexpr (VERIFY) flag_mismatch(a.mismatch, bad != 0);
         return;
@@ -1672,11 +1676,12 @@ __global__ void __launch_bounds__(256, 4) k_enc_lds(EncodeArgs a) {
         const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
         const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
         const ChunkIn in{a, row0, cnt, soff, tile};
-        if (c == 0) lds_transform<F, true, LOGM>(acc, cnt, tw, NoNeed{}, in, LdsIO<F>{acc});
-        else lds_transform<F, true, LOGM>(cur, cnt, tw, NoNeed{}, in, AccXor{acc});
+        if (c == 0) lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, 32, NT>(acc, cnt, tw, NoNeed{}, in, LdsIO<F>{acc});
+        else lds_transform<F, true, LOGM, ChunkIn, AccXor, NoNeed, 0, 32, NT>(cur, cnt, tw, NoNeed{}, in, AccXor{acc});
     }
     uint32_t bad = 0;
-    lds_transform<F, false, LOGM>(acc, a.p, a.tw_fft, NoNeed{}, LdsIO<F>{acc}, ParityOut{a, soff, tile, &bad});
+    lds_transform<F, false, LOGM, LdsIO<F>, ParityOut, NoNeed, 0, 32, NT>(acc, a.p, a.tw_fft, NoNeed{}, LdsIO<F>{acc},
+                                                                    ParityOut{a, soff, tile, &bad});
     if constexpr (VERIFY) {
         flag_mismatch(a.mismatch, bad != 0);
     }
@@ -1735,12 +1740,12 @@ hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
 
 template <class F, int LOGM, class FT>
 hipError_t enc_lds_tt(bool verify, const EncodeArgs &a, hipStream_t s) {
-    const dim3 grid((unsigned)((a.shard_size + LTile<F>::TB - 1) / LTile<F>::TB), (unsigned)a.nstripes);
+    const dim3 grid((unsigned)((a.shard_size + LTile<F>::TB - 1) / LTile<F>::TB), (unsigned)a.nstripes), block(enc_threads<LOGM>());
     const size_t lds = (size_t)(enc_acc_regs(LOGM) ? 1 : 2) * (1 << LOGM) * LTile<F>::ROW;
     auto go = [&](auto vf, auto sf) {
         constexpr bool V = decltype(vf)::value, IS = decltype(sf)::value;
         (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, V, FT, IS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((k_enc_lds<F, LOGM, V, FT, IS>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_enc_lds<F, LOGM, V, FT, IS>), grid, block, lds, s, a);
     };
     const bool isub = !std::is_same<F, FT>::value && a.tw_ifft_sub && a.ifft_nff;
     if constexpr (!std::is_same<F, FT>::value) {
@@ -1779,6 +1784,12 @@ hipError_t enc_lds_f(int logm, bool verify, const EncodeArgs &a, hipStream_t s) 
         case 6: return enc_lds_t<F, 6>(verify, a, s);
         case 7: return enc_lds_t<F, 7>(verify, a, s);
         case 8: return enc_lds_t<F, 8>(verify, a, s);
+    }
+    if constexpr (std::is_same<F, F16<2>>::value) {  // m = 512, 1024: 64-byte tiles only
+        switch (logm) {
+            case 9: return enc_lds_t<F, 9>(verify, a, s);
+            case 10: return enc_lds_t<F, 10>(verify, a, s);
+        }
     }
     return hipErrorInvalidValue;
 }
@@ -1977,6 +1988,7 @@ hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStr
 }
 
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s) {
+    if (logm > 8) return bits == 16 ? enc_lds_f<F16<2>>(logm, verify, a, s) : hipErrorInvalidValue;
     const bool narrow = pick_narrow((a.shard_size + 127) / 128 * (uint64_t)a.nstripes < kLdsMinGrid);
     if (narrow) return bits == 16 ? enc_lds_f<F16<2>>(logm, verify, a, s) : enc_lds_f<F8<2>>(logm, verify, a, s);
     return bits == 16 ? enc_lds_f<F16<4>>(logm, verify, a, s) : enc_lds_f<F8<4>>(logm, verify, a, s);

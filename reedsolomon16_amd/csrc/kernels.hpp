@@ -161,7 +161,9 @@ hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStr
 // m + k <= 160 (its LDS image).
 bool rec_bs256_available(int bits, int logn, bool sub, int mtrunc);
 hipError_t launch_rec_bs256(const RecArgs &a, hipStream_t s);
-// Encode (or verify) for 2 <= logm <= 8, twiddles as for launch_encode_reg.
+// Encode (or verify) for 2 <= logm <= 8, and GF(2^16) up to kMaxLdsEncLogM16
+// (64-byte tiles), twiddles as for launch_encode_reg.
+constexpr int kMaxLdsEncLogM16 = 10;
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 
 

@@ -36,6 +36,11 @@ CONFIGS = {
     # 256 erasures, one stripe and one pattern over 8 stripes per launch
     "C5r": (16, 1024, 256, 256 << 10, "reconstruct"),
     "C5rb8": (16, 1024, 256, 256 << 10, "reconstruct", 8),
+    # m = 512 / 1024 encodes (the reference's 1000- and 5000-shard tests' geometries, larger rows)
+    "L512": (16, 700, 300, 256 << 10, "encode"),
+    "L1024": (16, 4000, 1000, 64 << 10, "encode"),
+    "L1024b4": (16, 4000, 1000, 64 << 10, "encode", 4),
+    "L1024v": (16, 4000, 1000, 64 << 10, "verify"),
 }
 # Host-resident (PCIe-inclusive) variants: shards in host memory, rs_encode /
 # rs_reconstruct stream them through the GPU.  "p" = pinned rows (rs_host_alloc).

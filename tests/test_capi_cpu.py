@@ -140,7 +140,10 @@ def test_constructor_errors():
     assert rs.New16(10, 1).encode_path == "reg16-m1"
     assert rs.New16(1024, 256).encode_path == "lds-m256"
     assert rs.New16(96, 100).encode_path == "lds-m128"
-    assert rs.New16(1024, 300).encode_path == "multipass"
+    # m = 512, 1024 (GF(2^16)): the LDS encode with 64-byte tiles; m = 2048: multi-pass
+    assert rs.New16(1024, 300).encode_path == "lds-m512"
+    assert rs.New16(4000, 1000).encode_path == "lds-m1024"
+    assert rs.New16(3000, 1025).encode_path == "multipass"
 
 
 def test_debug_set_path_knobs(paths):
