@@ -521,10 +521,11 @@ int build_decode_plan(rs_codec *c) {
 }
 
 // One LDS-resident reconstruct launch covers n <= 256 (both fields) and, for
-// GF(2^16), n up to 2048 (64-byte tiles, kernels.hpp kMaxLdsRecLogN16); larger
-// n runs the multi-pass kernels.
+// GF(2^16), n up to 4096 (64-byte tiles to 2048, half tiles at 4096,
+// kernels.hpp kMaxLdsRecLogN16); larger n runs the multi-pass kernels.
 bool rec_lds_ok(const rs_codec *c) {
-    return c->logn <= kMaxLdsLogN || (c->bits == 16 && c->logn <= kMaxLdsRecLogN16);
+    return c->logn <= kMaxLdsLogN ||
+           (c->bits == 16 && (c->logn <= 11 || (c->logn <= kMaxLdsRecLogN16 && g_path_lds_big.load(std::memory_order_relaxed))));
 }
 
 hipStream_t pick_stream(rs_codec *c, void *s) {

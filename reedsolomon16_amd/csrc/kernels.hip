@@ -1337,7 +1337,11 @@ struct LdsPsi {
 template <int LOGN> constexpr int rec_lds_threads() { return LOGN >= 10 ? 1024 : 256; }
 // PKV = 2 (half tiles, n >= 1024): two 512-thread workgroups per CU, so one
 // workgroup's pass barriers are covered by the other's work.
-template <int LOGN, int PKV> constexpr int rec_threads() { return PKV == 2 ? 512 : rec_lds_threads<LOGN>(); }
+// n = 4096 (round 6): half tiles only (the 4096 x 32-byte image is 128 KB),
+// one 1024-thread workgroup per CU.
+template <int LOGN, int PKV> constexpr int rec_threads() {
+    return PKV == 2 ? (LOGN >= 12 ? 1024 : 512) : rec_lds_threads<LOGN>();
+}
 
 // n = 512..2048 with BSUB: the transforms in subfield coordinates wherever
 // every twiddle of a pass lies in GF(2^8) (rec_big_sub_passes; RecArgs::tw_*_sub).
@@ -1347,7 +1351,7 @@ template <int LOGN> struct BigSub {
 };
 
 template <class F, class FT, int LOGN, bool BSUB = false, int PKV = 1>
-__global__ void __launch_bounds__((rec_threads<LOGN, PKV>()), (PKV == 2 ? 2 : 1)) k_rec_lds(RecArgs a) {
+__global__ void __launch_bounds__((rec_threads<LOGN, PKV>()), (PKV == 2 && LOGN < 12 ? 2 : 1)) k_rec_lds(RecArgs a) {
     typedef LTile<F, PKV> L;  // packed 64-byte tiles (LTile PK), or half tiles (PKV = 2)
     typedef typename F::Vec V;
     constexpr int N = 1 << LOGN, U = L::U, NT = rec_threads<LOGN, PKV>();
@@ -1704,15 +1708,20 @@ hipError_t rec_lds_tb(const RecArgs &a, hipStream_t s) {
 template <class F, class FT, int LOGN>
 hipError_t rec_lds_t(const RecArgs &a, hipStream_t s) {
     if constexpr (LOGN >= 10 && std::is_same<F, F16<2>>::value) {
-        // n = 1024, 2048: half tiles, two workgroups per CU (rs_debug_set_path "rec_half")
-        if (rec_half_enabled()) {
+        // n = 1024, 2048: half tiles, two workgroups per CU (rs_debug_set_path "rec_half");
+        // n = 4096: half tiles always
+        if (LOGN >= 12 || rec_half_enabled()) {
             if (a.tw_ifft_sub && a.tw_fft_sub && a.tw_dmap) return rec_lds_tb<F, FT, LOGN, true, 2>(a, s);
             return rec_lds_tb<F, FT, LOGN, false, 2>(a, s);
         }
     }
-    if constexpr (LOGN > 8)
-        if (a.tw_ifft_sub && a.tw_fft_sub && a.tw_dmap) return rec_lds_tb<F, FT, LOGN, true>(a, s);
-    return rec_lds_tb<F, FT, LOGN, false>(a, s);
+    if constexpr (LOGN >= 12) {
+        return hipErrorInvalidValue;  // (unreachable: half tiles above)
+    } else {
+        if constexpr (LOGN > 8)
+            if (a.tw_ifft_sub && a.tw_fft_sub && a.tw_dmap) return rec_lds_tb<F, FT, LOGN, true>(a, s);
+        return rec_lds_tb<F, FT, LOGN, false>(a, s);
+    }
 }
 template <class F, class FT = F>
 hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
@@ -1726,13 +1735,14 @@ hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
         case 7: return rec_lds_t<F, FT, 7>(a, s);
         case 8: return rec_lds_t<F, FT, 8>(a, s);
     }
-    // n = 512 .. 2048: GF(2^16) in full-field coordinates, 64-byte tiles (the
-    // n x 80-byte image fills the 160 KB LDS at n = 2048)
+    // n = 512 .. 2048: GF(2^16), 64-byte tiles (the packed n x 64-byte image
+    // takes 128 KB at n = 2048); n = 4096: 32-byte half tiles (128 KB)
     if constexpr (std::is_same<F, F16<2>>::value && std::is_same<FT, F>::value) {
         switch (logn) {
             case 9: return rec_lds_t<F, FT, 9>(a, s);
             case 10: return rec_lds_t<F, FT, 10>(a, s);
             case 11: return rec_lds_t<F, FT, 11>(a, s);
+            case 12: return rec_lds_t<F, FT, 12>(a, s);
         }
     }
     return hipErrorInvalidValue;

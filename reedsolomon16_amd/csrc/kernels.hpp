@@ -53,7 +53,7 @@ struct EncodeArgs {
 // passes before big_sub_fft_end(logn) run in GF(2^8)-subfield coordinates.
 // The host (codec.cpp upload_big_sub) checks every twiddle slot of exactly
 // these passes against the schedule, so both sides share these definitions.
-constexpr int big_sub_ifft_first(int logn) { return logn == 11 ? 2 : 1; }
+constexpr int big_sub_ifft_first(int logn) { return logn >= 11 ? 2 : 1; }
 constexpr int big_sub_fft_end(int logn) { return (void)logn, 4; }
 
 // Test-only kernel-path overrides (rs_debug_set_path, codec.cpp): the LDS /
@@ -152,8 +152,9 @@ struct RecArgs {
 };
 // sub: GF(2^16) transforms in subfield coordinates (tw_ifft/tw_fft are
 // kTwDwords8 subfield tables; tw_in/tw_out fold in the coordinate change).
-// logn <= 8, or GF(2^16) with logn <= kMaxLdsRecLogN16 (full field, need_w / rev set).
-constexpr int kMaxLdsRecLogN16 = 11;
+// logn <= 8, or GF(2^16) with logn <= kMaxLdsRecLogN16 (full field, need_w / rev set;
+// n = 4096 in 32-byte half tiles, 1024 threads).
+constexpr int kMaxLdsRecLogN16 = 12;
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s);
 // Bit-sliced reconstruct (csrc/bitslice_dec.hip): GF(2^16), n = 256, transforms
 // in subfield coordinates (tw_ifft / tw_fft: kTwDwords8 subfield tables,

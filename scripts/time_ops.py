@@ -41,6 +41,9 @@ CONFIGS = {
     "L1024": (16, 4000, 1000, 64 << 10, "encode"),
     "L1024b4": (16, 4000, 1000, 64 << 10, "encode", 4),
     "L1024v": (16, 4000, 1000, 64 << 10, "verify"),
+    # n = 4096 reconstruct (3000 + 1000: 1000 erasures; 2100 + 10: 10 erasures)
+    "R4096": (16, 3000, 1000, 64 << 10, "reconstruct"),
+    "R4096e10": (16, 2100, 10, 256 << 10, "reconstruct"),
 }
 # Host-resident (PCIe-inclusive) variants: shards in host memory, rs_encode /
 # rs_reconstruct stream them through the GPU.  "p" = pinned rows (rs_host_alloc).

@@ -154,7 +154,7 @@ def test_multi_async_tickets_match_single_codec():
 @pytest.mark.parametrize("bits,k,p,S,devs", [(16, 128, 32, 64 * 7, [0, 0, 0]), (16, 10, 4, 64, DEV4),
                                              (8, 10, 4, 64 * 5, [0] * 8), (16, 300, 100, 64 * 9, [0, 0]),
                                              (8, 100, 28, 64 * 33, DEV4),
-                                             (16, 2000, 100, 64 * 3, [0, 0])])  # n = 4096: multi-pass reconstruct on each part
+                                             (16, 2000, 100, 64 * 3, [0, 0])])  # n = 4096: one LDS reconstruct (half tiles) on each part
 def test_multi_ragged_splits(bits, k, p, S, devs):
     """Shard sizes the parts split unevenly, or that leave parts empty."""
     rng = np.random.default_rng(k + S)

@@ -1,11 +1,12 @@
-"""GPU parity of the LDS-resident reconstruct for n = 512 .. 2048 work rows
-(kernels.hip k_rec_lds<F16<2>, F16<2>, 9..11>: 64-byte column tiles of all n
-rows in LDS, the revealed-row mask and output indices from HBM), the C5 repair
+"""GPU parity of the LDS-resident reconstruct for n = 512 .. 4096 work rows
+(kernels.hip k_rec_lds<F16<2>, F16<2>, 9..12>: 64-byte column tiles of all n
+rows in LDS, 32-byte half tiles at n = 4096, the revealed-row mask and output
+indices from HBM), the C5 repair
 geometry (1024 + 256, n = 2048) among them, against the oracle's
 reconstruct (leopard16.go:390-570) bit for bit: erasure classes (random at
 the limit, data only, parity only, a few rows, one row), recover_all on and
 off, strided and row-list launches, batched stripes, the host-pointer path,
-and the multi-pass kernels past n = 2048."""
+and the multi-pass kernels past n = 4096."""
 import numpy as np
 import pytest
 
@@ -54,8 +55,9 @@ def oracle_rec(k, p, full, mask, recover_all):
     return ref
 
 
-# (k, p, S): n = 512 (m = 128), n = 1024, n = 2048 (C5 geometry and a ragged one)
-GEOMS = [(300, 100, 192), (700, 200, 128), (1024, 256, 128), (1000, 200, 64)]
+# (k, p, S): n = 512 (m = 128), n = 1024, n = 2048 (C5 geometry and a ragged
+# one), n = 4096 (m = 1024, and m = 16 with 2100 data shards)
+GEOMS = [(300, 100, 192), (700, 200, 128), (1024, 256, 128), (1000, 200, 64), (3000, 1000, 64), (2100, 10, 128)]
 
 
 @pytest.mark.parametrize("k,p,S", GEOMS)
@@ -112,9 +114,9 @@ def test_big_n_row_list_and_batch(torch):
         assert np.array_equal(slab[z].cpu().numpy(), fulls[z]), z
 
 
-def test_big_n_host_reconstruct(torch):
-    """Host shards (rs_reconstruct through the staging pipeline) with n = 2048."""
-    k, p, S = 1024, 256, 4096
+@pytest.mark.parametrize("k,p,S", [(1024, 256, 4096), (2500, 900, 64 * 20)])
+def test_big_n_host_reconstruct(torch, k, p, S):
+    """Host shards (rs_reconstruct through the staging pipeline) with n = 2048 and 4096."""
     full = encoded(k, p, S, 9)
     er = patterns(k, p, 10)["random_p"]
     c = rs.New16(k, p)
@@ -124,11 +126,15 @@ def test_big_n_host_reconstruct(torch):
         assert np.array_equal(sh[i], full[i]), i
 
 
-def test_multipass_past_2048(torch):
-    """n = 4096 (2100 + 10: m = 16) still runs the multi-pass kernels."""
-    k, p, S = 2100, 10, 64
+@pytest.mark.parametrize("k,p,lds", [(2100, 10, 1), (2100, 10, 0), (4000, 1000, 1)])
+def test_n4096_lds_and_multipass(torch, paths, k, p, lds):
+    """n = 4096 (2100 + 10: m = 16) in one LDS launch and through the
+    multi-pass kernels (rs_debug_set_path "lds_big" 0); n = 8192 (the
+    reference's 4000 + 1000, reedsolomon_test.go:82) multi-pass."""
+    S = 64
+    paths("lds_big", lds)
     full = encoded(k, p, S, 11)
-    er = np.array([0, 1, 700, 2099, 2100, 2109, 1500, 33, 1024, 2048])
+    er = np.array([0, 1, 700, 2099, 2100, k + p - 1, 1500, 33, 1024, 2048])
     mask = np.zeros(k + p, bool)
     mask[er] = True
     ref = oracle_rec(k, p, full, mask, True)
