@@ -363,7 +363,7 @@ bool rs::rec_half_enabled() { return g_path_rec_half.load(std::memory_order_rela
 namespace {
 
 // One LDS-resident encode launch covers m <= 256 (both fields) and, for
-// GF(2^16), m up to 1024 (64-byte tiles, kernels.hpp kMaxLdsEncLogM16);
+// GF(2^16), m up to 2048 (64-byte tiles, half tiles at 2048, kernels.hpp kMaxLdsEncLogM16);
 // larger m runs the multi-pass kernels.
 bool enc_lds_ok(const rs_codec *c) {
     return c->logm <= kMaxLdsLogN ||
@@ -521,8 +521,8 @@ int build_decode_plan(rs_codec *c) {
 }
 
 // One LDS-resident reconstruct launch covers n <= 256 (both fields) and, for
-// GF(2^16), n up to 4096 (64-byte tiles to 2048, half tiles at 4096,
-// kernels.hpp kMaxLdsRecLogN16); larger n runs the multi-pass kernels.
+// GF(2^16), n up to 8192 (64-byte tiles to 2048, half tiles at 4096, quarter
+// tiles at 8192, kernels.hpp kMaxLdsRecLogN16); larger n runs the multi-pass kernels.
 bool rec_lds_ok(const rs_codec *c) {
     return c->logn <= kMaxLdsLogN ||
            (c->bits == 16 && (c->logn <= 11 || (c->logn <= kMaxLdsRecLogN16 && g_path_lds_big.load(std::memory_order_relaxed))));

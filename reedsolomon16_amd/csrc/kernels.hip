@@ -1083,12 +1083,14 @@ bool pick_narrow(bool automatic) {
 // block, j = the tile's half), so the n x 32-byte image (64 KB at n = 2048)
 // lets two workgroups share a CU.  The caller addresses a half tile from its
 // block (tile = block * 64) and adds the half's unit offset (2j) to u.
+// PK = 4 (n = 8192): quarter tiles, one 16-byte unit (symbols 8j .. 8j + 7)
+// of a row per workgroup, the 8192 x 16-byte image 128 KB.
 template <class F, int PK = 0>
 struct LTile {
     static_assert(!F::SYM16 || F::W >= 2, "a GF(2^16) LDS tile must cover whole 64-byte blocks (W >= 2)");
-    static_assert(PK != 2 || (F::SYM16 && F::W == 2), "half tiles: GF(2^16) 16-byte units");
+    static_assert(PK < 2 || (F::SYM16 && F::W == 2), "half / quarter tiles: GF(2^16) 16-byte units");
     static constexpr bool W16 = F::SYM16;
-    static constexpr int TB = (PK == 2 ? 16 : 32) * F::W;  // bytes of each row owned by a workgroup
+    static constexpr int TB = (PK == 4 ? 8 : PK == 2 ? 16 : 32) * F::W;  // bytes of each row owned by a workgroup
     static constexpr bool PACK = PK != 0 && W16 && F::W == 2;
     static constexpr int ROW = PACK ? TB : TB + 16;  // LDS row stride
     static constexpr int UB = W16 ? 8 * F::W : 4 * F::W;  // global bytes per unit
@@ -1340,7 +1342,7 @@ template <int LOGN> constexpr int rec_lds_threads() { return LOGN >= 10 ? 1024 :
 // n = 4096 (round 6): half tiles only (the 4096 x 32-byte image is 128 KB),
 // one 1024-thread workgroup per CU.
 template <int LOGN, int PKV> constexpr int rec_threads() {
-    return PKV == 2 ? (LOGN >= 12 ? 1024 : 512) : rec_lds_threads<LOGN>();
+    return PKV == 4 ? 1024 : PKV == 2 ? (LOGN >= 12 ? 1024 : 512) : rec_lds_threads<LOGN>();
 }
 
 // n = 512..2048 with BSUB: the transforms in subfield coordinates wherever
@@ -1352,16 +1354,17 @@ template <int LOGN> struct BigSub {
 
 template <class F, class FT, int LOGN, bool BSUB = false, int PKV = 1>
 __global__ void __launch_bounds__((rec_threads<LOGN, PKV>()), (PKV == 2 && LOGN < 12 ? 2 : 1)) k_rec_lds(RecArgs a) {
-    typedef LTile<F, PKV> L;  // packed 64-byte tiles (LTile PK), or half tiles (PKV = 2)
+    typedef LTile<F, PKV> L;  // packed 64-byte tiles (LTile PK), or half / quarter tiles (PKV = 2 / 4)
     typedef typename F::Vec V;
     constexpr int N = 1 << LOGN, U = L::U, NT = rec_threads<LOGN, PKV>();
     constexpr int K = (N * U + NT - 1) / NT;  // derivative outputs per thread
     __shared__ __attribute__((aligned(16))) uint8_t lds[N * L::ROW];
     uint32_t bx = blockIdx.x;
-    if constexpr (PKV == 2) {
-        // half tiles: the four tiles of a 128-byte line go to one XCD: blocks
-        // 32q + x + 8j (j < 4) take tiles 32q + 4x + j
-        if (bx < (gridDim.x & ~31u)) bx = (bx & ~31u) | ((bx & 7u) << 2) | ((bx >> 3) & 3u);
+    if constexpr (PKV >= 2) {
+        // half (quarter) tiles: the T = 2 PKV tiles of a 128-byte line go to one
+        // XCD: blocks 8Tq + x + 8j (j < T) take tiles 8Tq + Tx + j
+        constexpr uint32_t T = 2 * PKV, G = 8 * T;
+        if (bx < (gridDim.x & ~(G - 1))) bx = (bx & ~(G - 1)) | ((bx & 7u) * T) | ((bx >> 3) & (T - 1));
     } else if constexpr (LOGN > 8) {
         // 64-byte tiles: the two tiles of a 128-byte line go to one XCD
         // (workgroups are dealt round-robin over the 8 XCDs, each with its own
@@ -1369,8 +1372,8 @@ __global__ void __launch_bounds__((rec_threads<LOGN, PKV>()), (PKV == 2 && LOGN 
         if (bx < (gridDim.x & ~15u)) bx = (bx & ~15u) | ((bx & 7u) << 1) | ((bx >> 3) & 1u);
     }
     // a half tile is addressed from its 64-byte block, its units from uo on
-    const uint64_t tile = PKV == 2 ? (uint64_t)(bx >> 1) * 64 : (uint64_t)bx * L::TB;
-    const int uo = PKV == 2 ? 2 * (int)(bx & 1u) : 0;
+    const uint64_t tile = PKV >= 2 ? (uint64_t)(bx / PKV) * 64 : (uint64_t)bx * L::TB;
+    const int uo = PKV >= 2 ? L::U * (int)(bx % PKV) : 0;
     uint8_t *const sbase = a.base ? a.base + (uint64_t)blockIdx.y * a.stripe_stride : nullptr;  // this stripe
     // work row r = present shard * errLocs[r] (mulgf16 through the table), or 0.
     // Branch-free, so the four rows of a first-pass item issue their loads
@@ -1557,25 +1560,36 @@ __global__ void __launch_bounds__((rec_threads<LOGN, PKV>()), (PKV == 2 && LOGN 
 // ISUB: the chunk IFFTs' subfield passes (EncodeArgs::tw_ifft_sub; needs FT = F16S).
 // m = 512, 1024 (GF(2^16), round 6): 64-byte tiles (F16<2>) and one
 // 1024-thread workgroup per CU, the m x 80-byte image(s) taking 80 KB of LDS
-// (m = 1024: acc in registers, one image; m = 512: acc and chunk images).
+// (m = 1024: acc in registers, one image; m = 512: acc and chunk images);
+// m = 2048: 32-byte half tiles (LTile PK = 2), acc and chunk images 128 KB.
 template <int LOGM> constexpr int enc_threads() { return LOGM >= 9 ? 1024 : 256; }
+template <int LOGM> constexpr int enc_pk() { return LOGM >= 11 ? 2 : 0; }
 template <class F, int LOGM, bool VERIFY, class FT = F, bool ISUB = false>
 __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_enc_lds(EncodeArgs a) {
-    typedef LTile<F> L;
+    constexpr int PK = enc_pk<LOGM>();
+    typedef LTile<F, PK> L;
     typedef typename F::Vec V;
     constexpr int M = 1 << LOGM, NT = enc_threads<LOGM>();
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
     constexpr bool ACCR = enc_acc_regs(LOGM);
     uint8_t *acc = lds_dyn, *cur = ACCR ? lds_dyn : lds_dyn + M * L::ROW;
-    const uint64_t tile = (uint64_t)blockIdx.x * L::TB;
+    uint32_t bx = blockIdx.x;
+    if constexpr (PK == 2) {
+        // half tiles: the four tiles of a 128-byte line go to one XCD (as k_rec_lds)
+        if (bx < (gridDim.x & ~31u)) bx = (bx & ~31u) | ((bx & 7u) << 2) | ((bx >> 3) & 3u);
+    }
+    // a half tile is addressed from its 64-byte block, its units from uo on
+    const uint64_t tile = PK == 2 ? (uint64_t)(bx >> 1) * 64 : (uint64_t)bx * L::TB;
+    const int uo = PK == 2 ? L::U * (int)(bx & 1u) : 0;
     const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
     constexpr int its = ifft_slot_count(LOGM);
     struct ChunkIn {
         const EncodeArgs &a;
         int row0, cnt;
         uint64_t soff, tile;
+        int uo;
         __device__ V operator()(int r, int u) const {
-            if (r < cnt && L::valid(tile, a.shard_size, u)) return F::load(row_ptr(a.data, row0 + r) + soff + tile, u);
+            if (r < cnt && L::valid(tile, a.shard_size, u)) return F::load(row_ptr(a.data, row0 + r) + soff + tile, u + uo);
             return F::zero();
         }
     };
@@ -1591,14 +1605,15 @@ __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_
     struct ParityOut {
         const EncodeArgs &a;
         uint64_t soff, tile;
+        int uo;
         uint32_t *bad;
         __device__ void operator()(int r, int u, const V &v0) const {
             if (r >= a.p || !L::valid(tile, a.shard_size, u)) return;
             V v = v0;
             if constexpr (SUB) sub_swap<F>(v, a.tw_dmap);  // back to (lo, hi)
             uint8_t *prow = row_ptr(a.parity, r) + soff + tile;
-            if constexpr (VERIFY) *bad |= F::diff(v, F::load(prow, u));
-            else F::store(prow, u, v);
+            if constexpr (VERIFY) *bad |= F::diff(v, F::load(prow, u + uo));
+            else F::store(prow, u + uo, v);
         }
     };
     if constexpr (ACCR) {
@@ -1622,7 +1637,7 @@ __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_
             const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
             const uint32_t *tws = isub ? a.tw_ifft_sub + (uint64_t)c * its * FT::TWD : nullptr;
             const LdsIO<F> lio{cur};
-            const ChunkIn in{a, row0, cnt, soff, tile};
+            const ChunkIn in{a, row0, cnt, soff, tile, uo};
             if constexpr (isub) {
                 // full-field passes, the last one writing subfield coordinates, then subfield passes
                 const LdsPsi<F> psi{cur, a.tw_dmap};
@@ -1672,20 +1687,20 @@ __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_
         }
         __syncthreads();
         lds_transform<FT, false, LOGM, LdsIO<FT>, ParityOut, NoNeed, 1, 32, NT>(cur, a.p, twf, NoNeed{}, LdsIO<FT>{cur},
-                                                                         ParityOut{a, soff, tile, &bad});
+                                                                         ParityOut{a, soff, tile, uo, &bad});
         if constexpr (VERIFY) flag_mismatch(a.mismatch, bad != 0);
         return;
     }
     for (int c = 0; c < a.nchunks; c++) {
         const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
         const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
-        const ChunkIn in{a, row0, cnt, soff, tile};
-        if (c == 0) lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, 32, NT>(acc, cnt, tw, NoNeed{}, in, LdsIO<F>{acc});
-        else lds_transform<F, true, LOGM, ChunkIn, AccXor, NoNeed, 0, 32, NT>(cur, cnt, tw, NoNeed{}, in, AccXor{acc});
+        const ChunkIn in{a, row0, cnt, soff, tile, uo};
+        if (c == 0) lds_transform<F, true, LOGM, ChunkIn, LdsIO<F, PK>, NoNeed, 0, 32, NT, false, PK>(acc, cnt, tw, NoNeed{}, in, LdsIO<F, PK>{acc});
+        else lds_transform<F, true, LOGM, ChunkIn, AccXor, NoNeed, 0, 32, NT, false, PK>(cur, cnt, tw, NoNeed{}, in, AccXor{acc});
     }
     uint32_t bad = 0;
-    lds_transform<F, false, LOGM, LdsIO<F>, ParityOut, NoNeed, 0, 32, NT>(acc, a.p, a.tw_fft, NoNeed{}, LdsIO<F>{acc},
-                                                                    ParityOut{a, soff, tile, &bad});
+    lds_transform<F, false, LOGM, LdsIO<F, PK>, ParityOut, NoNeed, 0, 32, NT, false, PK>(acc, a.p, a.tw_fft, NoNeed{}, LdsIO<F, PK>{acc},
+                                                                    ParityOut{a, soff, tile, uo, &bad});
     if constexpr (VERIFY) {
         flag_mismatch(a.mismatch, bad != 0);
     }
@@ -1707,7 +1722,11 @@ hipError_t rec_lds_tb(const RecArgs &a, hipStream_t s) {
 }
 template <class F, class FT, int LOGN>
 hipError_t rec_lds_t(const RecArgs &a, hipStream_t s) {
-    if constexpr (LOGN >= 10 && std::is_same<F, F16<2>>::value) {
+    if constexpr (LOGN >= 13 && std::is_same<F, F16<2>>::value) {  // n = 8192: quarter tiles
+        if (a.tw_ifft_sub && a.tw_fft_sub && a.tw_dmap) return rec_lds_tb<F, FT, LOGN, true, 4>(a, s);
+        return rec_lds_tb<F, FT, LOGN, false, 4>(a, s);
+    }
+    if constexpr (LOGN >= 10 && LOGN < 13 && std::is_same<F, F16<2>>::value) {
         // n = 1024, 2048: half tiles, two workgroups per CU (rs_debug_set_path "rec_half");
         // n = 4096: half tiles always
         if (LOGN >= 12 || rec_half_enabled()) {
@@ -1736,13 +1755,15 @@ hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
         case 8: return rec_lds_t<F, FT, 8>(a, s);
     }
     // n = 512 .. 2048: GF(2^16), 64-byte tiles (the packed n x 64-byte image
-    // takes 128 KB at n = 2048); n = 4096: 32-byte half tiles (128 KB)
+    // takes 128 KB at n = 2048); n = 4096: 32-byte half tiles (128 KB);
+    // n = 8192: 16-byte quarter tiles (128 KB)
     if constexpr (std::is_same<F, F16<2>>::value && std::is_same<FT, F>::value) {
         switch (logn) {
             case 9: return rec_lds_t<F, FT, 9>(a, s);
             case 10: return rec_lds_t<F, FT, 10>(a, s);
             case 11: return rec_lds_t<F, FT, 11>(a, s);
             case 12: return rec_lds_t<F, FT, 12>(a, s);
+            case 13: return rec_lds_t<F, FT, 13>(a, s);
         }
     }
     return hipErrorInvalidValue;
@@ -1750,8 +1771,9 @@ hipError_t rec_lds_f(int logn, const RecArgs &a, hipStream_t s) {
 
 template <class F, int LOGM, class FT>
 hipError_t enc_lds_tt(bool verify, const EncodeArgs &a, hipStream_t s) {
-    const dim3 grid((unsigned)((a.shard_size + LTile<F>::TB - 1) / LTile<F>::TB), (unsigned)a.nstripes), block(enc_threads<LOGM>());
-    const size_t lds = (size_t)(enc_acc_regs(LOGM) ? 1 : 2) * (1 << LOGM) * LTile<F>::ROW;
+    typedef LTile<F, enc_pk<LOGM>()> L;
+    const dim3 grid((unsigned)((a.shard_size + L::TB - 1) / L::TB), (unsigned)a.nstripes), block(enc_threads<LOGM>());
+    const size_t lds = (size_t)(enc_acc_regs(LOGM) ? 1 : 2) * (1 << LOGM) * L::ROW;
     auto go = [&](auto vf, auto sf) {
         constexpr bool V = decltype(vf)::value, IS = decltype(sf)::value;
         (void)hipFuncSetAttribute((const void *)k_enc_lds<F, LOGM, V, FT, IS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1795,10 +1817,11 @@ hipError_t enc_lds_f(int logm, bool verify, const EncodeArgs &a, hipStream_t s) 
         case 7: return enc_lds_t<F, 7>(verify, a, s);
         case 8: return enc_lds_t<F, 8>(verify, a, s);
     }
-    if constexpr (std::is_same<F, F16<2>>::value) {  // m = 512, 1024: 64-byte tiles only
+    if constexpr (std::is_same<F, F16<2>>::value) {  // m = 512, 1024: 64-byte tiles; 2048: half tiles
         switch (logm) {
             case 9: return enc_lds_t<F, 9>(verify, a, s);
             case 10: return enc_lds_t<F, 10>(verify, a, s);
+            case 11: return enc_lds_t<F, 11>(verify, a, s);
         }
     }
     return hipErrorInvalidValue;

@@ -53,7 +53,7 @@ struct EncodeArgs {
 // passes before big_sub_fft_end(logn) run in GF(2^8)-subfield coordinates.
 // The host (codec.cpp upload_big_sub) checks every twiddle slot of exactly
 // these passes against the schedule, so both sides share these definitions.
-constexpr int big_sub_ifft_first(int logn) { return logn >= 11 ? 2 : 1; }
+constexpr int big_sub_ifft_first(int logn) { return logn >= 13 ? 3 : logn >= 11 ? 2 : 1; }
 constexpr int big_sub_fft_end(int logn) { return (void)logn, 4; }
 
 // Test-only kernel-path overrides (rs_debug_set_path, codec.cpp): the LDS /
@@ -138,11 +138,11 @@ struct RecArgs {
     // is revealed; FFT groups whose rows are all unset are skipped.
     int prune;
     uint32_t need[8];           // n <= 256 rows
-    // n = 512 .. 2048 (GF(2^16), 64-byte tiles): the revealed-row mask as n / 32
+    // n = 512 .. 8192 (GF(2^16)): the revealed-row mask as n / 32
     // words and each work row's output index (-1: not revealed), both in HBM
     const uint32_t *need_w;
     const int *rev;
-    // n = 512 .. 2048, optional: subfield tables (kTwDwords8, zero where a slot
+    // n = 512 .. 8192, optional: subfield tables (kTwDwords8, zero where a slot
     // is full-field) of the passes kernels.hip BigSub<logn> runs in subfield
     // coordinates, and the coordinate-change map; nullptr: full field throughout
     const uint32_t *tw_ifft_sub, *tw_fft_sub, *tw_dmap;
@@ -153,8 +153,8 @@ struct RecArgs {
 // sub: GF(2^16) transforms in subfield coordinates (tw_ifft/tw_fft are
 // kTwDwords8 subfield tables; tw_in/tw_out fold in the coordinate change).
 // logn <= 8, or GF(2^16) with logn <= kMaxLdsRecLogN16 (full field, need_w / rev set;
-// n = 4096 in 32-byte half tiles, 1024 threads).
-constexpr int kMaxLdsRecLogN16 = 12;
+// n = 4096 / 8192 in 32-byte half / 16-byte quarter tiles, 1024 threads).
+constexpr int kMaxLdsRecLogN16 = 13;
 hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStream_t s);
 // Bit-sliced reconstruct (csrc/bitslice_dec.hip): GF(2^16), n = 256, transforms
 // in subfield coordinates (tw_ifft / tw_fft: kTwDwords8 subfield tables,
@@ -163,8 +163,8 @@ hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStr
 bool rec_bs256_available(int bits, int logn, bool sub, int mtrunc);
 hipError_t launch_rec_bs256(const RecArgs &a, hipStream_t s);
 // Encode (or verify) for 2 <= logm <= 8, and GF(2^16) up to kMaxLdsEncLogM16
-// (64-byte tiles), twiddles as for launch_encode_reg.
-constexpr int kMaxLdsEncLogM16 = 10;
+// (64-byte tiles, 32-byte half tiles at m = 2048), twiddles as for launch_encode_reg.
+constexpr int kMaxLdsEncLogM16 = 11;
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 
 

@@ -1,12 +1,13 @@
-"""GPU parity of the LDS-resident reconstruct for n = 512 .. 4096 work rows
-(kernels.hip k_rec_lds<F16<2>, F16<2>, 9..12>: 64-byte column tiles of all n
-rows in LDS, 32-byte half tiles at n = 4096, the revealed-row mask and output
+"""GPU parity of the LDS-resident reconstruct for n = 512 .. 8192 work rows
+(kernels.hip k_rec_lds<F16<2>, F16<2>, 9..13>: 64-byte column tiles of all n
+rows in LDS, 32-byte half tiles at n = 4096, 16-byte quarter tiles at n = 8192,
+the revealed-row mask and output
 indices from HBM), the C5 repair
 geometry (1024 + 256, n = 2048) among them, against the oracle's
 reconstruct (leopard16.go:390-570) bit for bit: erasure classes (random at
 the limit, data only, parity only, a few rows, one row), recover_all on and
 off, strided and row-list launches, batched stripes, the host-pointer path,
-and the multi-pass kernels past n = 4096."""
+and the multi-pass kernels (rs_debug_set_path "lds_big" 0)."""
 import numpy as np
 import pytest
 
@@ -56,8 +57,10 @@ def oracle_rec(k, p, full, mask, recover_all):
 
 
 # (k, p, S): n = 512 (m = 128), n = 1024, n = 2048 (C5 geometry and a ragged
-# one), n = 4096 (m = 1024, and m = 16 with 2100 data shards)
-GEOMS = [(300, 100, 192), (700, 200, 128), (1024, 256, 128), (1000, 200, 64), (3000, 1000, 64), (2100, 10, 128)]
+# one), n = 4096 (m = 1024, and m = 16 with 2100 data shards), n = 8192 (the
+# reference's 4000 + 1000, reedsolomon_test.go:82, and m = 128)
+GEOMS = [(300, 100, 192), (700, 200, 128), (1024, 256, 128), (1000, 200, 64), (3000, 1000, 64), (2100, 10, 128),
+         (4000, 1000, 64), (5000, 100, 128)]
 
 
 @pytest.mark.parametrize("k,p,S", GEOMS)
@@ -126,11 +129,11 @@ def test_big_n_host_reconstruct(torch, k, p, S):
         assert np.array_equal(sh[i], full[i]), i
 
 
-@pytest.mark.parametrize("k,p,lds", [(2100, 10, 1), (2100, 10, 0), (4000, 1000, 1)])
-def test_n4096_lds_and_multipass(torch, paths, k, p, lds):
-    """n = 4096 (2100 + 10: m = 16) in one LDS launch and through the
-    multi-pass kernels (rs_debug_set_path "lds_big" 0); n = 8192 (the
-    reference's 4000 + 1000, reedsolomon_test.go:82) multi-pass."""
+@pytest.mark.parametrize("k,p,lds", [(2100, 10, 1), (2100, 10, 0), (4000, 1000, 1), (4000, 1000, 0)])
+def test_n4096_n8192_lds_and_multipass(torch, paths, k, p, lds):
+    """n = 4096 (2100 + 10: m = 16) and n = 8192 (the reference's 4000 + 1000,
+    reedsolomon_test.go:82) in one LDS launch and through the multi-pass
+    kernels (rs_debug_set_path "lds_big" 0)."""
     S = 64
     paths("lds_big", lds)
     full = encoded(k, p, S, 11)
