@@ -386,7 +386,7 @@ void plan_encode_host(rs_codec *c) {
 // tw_ifft_sub): chunk c's twiddles are fftSkew[(c+1)m - 1 + ...]
 // (ifftDITEncoder leopard16.go:699-741), full-field in the first layers and
 // in GF(2^8) after them (C5, m = 256: layers 0-1 of every chunk and layer 2
-// of chunk 3 are full-field).  ifft_nff[c] = the first radix-4 pass from which
+// of chunk 3 are full-field; m = 1024: layers 0-2, 0-3, 0-3, 0-4).  ifft_nff[c] = the first radix-4 pass from which
 // every slot of the chunk lies in the subfield; the kernel needs the last
 // pass subfield (it is fused with the accumulator).
 int upload_ifft_sub(rs_codec *c) {
@@ -401,7 +401,8 @@ int upload_ifft_sub(rs_codec *c) {
         for (int p = 0; p < np; p++)
             for (int sl = passes[p].slot_off; sl < passes[p].slot_off + 3 * passes[p].groups; sl++)
                 if (lg[sl] != c->F->mod && !in_subfield(*c->F, lg[sl])) nff[ch] = std::max(nff[ch], p + 1);
-        if (nff[ch] > 2 || nff[ch] >= np) return RS_OK;  // the kernel compiles nff = 1 and 2
+        // the kernel compiles nff = 1 and 2 (and 3 for m >= 1024); the last pass is subfield
+        if (nff[ch] > (c->logm >= 10 ? 3 : 2) || nff[ch] >= np) return RS_OK;
         for (int sl = passes[nff[ch]].slot_off; sl < is; sl++)
             make_sub_twiddle(*c->F, lg[sl], ts.data() + ((size_t)ch * is + sl) * kTwDwords8);
     }
@@ -430,13 +431,22 @@ int ensure_device(rs_codec *c) {
             e = upload_split(c);
             if (e) return e;
         }
-        // m <= 256: every fftDIT twiddle is fftSkew[< 255], in GF(2^8)
-        bool sub = c->bits == 16 && c->logm > kMaxRegLogM && c->logm <= kMaxLdsLogN && c->logm % 2 == 0 &&
+        // m <= 256: every fftDIT twiddle is fftSkew[< 255], in GF(2^8); m = 1024:
+        // the FFT's passes before big_sub_fft_end (the rest, layers 0-1, are
+        // full-field and keep zero subfield tables; the kernel runs them full)
+        bool sub = c->bits == 16 && c->logm > kMaxRegLogM && c->logm <= kMaxLdsEncLogM16 && c->logm % 2 == 0 &&
                    sub_enabled() && sub_coords().ok;
-        for (uint32_t l : c->enc_fft_logs) sub = sub && in_subfield(*c->F, l);
+        size_t fsub_end = c->enc_fft_logs.size();  // slots [0, fsub_end) subfield
+        if (sub && c->logm > kMaxLdsLogN) {
+            const auto fp = fft_passes(c->logm);
+            const int fend = big_sub_fft_end(c->logm);
+            sub = (int)fp.size() > fend;
+            if (sub) fsub_end = fp[fend].slot_off;
+        }
+        for (size_t i = 0; i < fsub_end && sub; i++) sub = in_subfield(*c->F, c->enc_fft_logs[i]);
         if (sub) {
             std::vector<uint32_t> hf(std::max<size_t>(c->enc_fft_logs.size(), 1) * kTwDwords8, 0), dm(kTwDwords8, 0);
-            for (size_t i = 0; i < c->enc_fft_logs.size(); i++) make_sub_twiddle(*c->F, c->enc_fft_logs[i], hf.data() + i * kTwDwords8);
+            for (size_t i = 0; i < fsub_end; i++) make_sub_twiddle(*c->F, c->enc_fft_logs[i], hf.data() + i * kTwDwords8);
             make_sub_dmap(dm.data());
             HIP_TRY(c->tw_fft_sub.ensure(hf.size()));
             HIP_TRY(c->tw_dmap.ensure(dm.size()));

@@ -1616,6 +1616,21 @@ __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_
             else F::store(prow, u + uo, v);
         }
     };
+    // m >= 512 (FSPLIT): the FFT's passes from FEND on are full-field, so its
+    // subfield passes end by writing normal coordinates back (LdsPsi) and the
+    // last pass stores through this sink, which converts nothing.
+    struct ParityOutFull {
+        const EncodeArgs &a;
+        uint64_t soff, tile;
+        int uo;
+        uint32_t *bad;
+        __device__ void operator()(int r, int u, const V &v) const {
+            if (r >= a.p || !L::valid(tile, a.shard_size, u)) return;
+            uint8_t *prow = row_ptr(a.parity, r) + soff + tile;
+            if constexpr (VERIFY) *bad |= F::diff(v, F::load(prow, u + uo));
+            else F::store(prow, u + uo, v);
+        }
+    };
     if constexpr (ACCR) {
         // acc in registers: the IFFT's last pass and the FFT's first are both
         // one radix-4 group at dist D = M/4 with the same item -> (rows, unit)
@@ -1642,12 +1657,22 @@ __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_
                 // full-field passes, the last one writing subfield coordinates, then subfield passes
                 const LdsPsi<F> psi{cur, a.tw_dmap};
                 const LdsIO<FT> lios{cur};
-                const int nff = a.ifft_nff[c];  // 1 or 2 (codec.cpp upload_ifft_sub)
+                // 1 or 2, and up to 3 for m = 1024 (codec.cpp upload_ifft_sub)
+                const int nff = a.ifft_nff[c];
                 if (nff == 1) lds_transform<F, true, LOGM, ChunkIn, LdsPsi<F>, NoNeed, 0, 1, NT, true>(cur, cnt, tw, NoNeed{}, in, psi);
                 else lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, 1, NT>(cur, cnt, tw, NoNeed{}, in, lio);
-                if (nff == 2) lds_transform<F, true, LOGM, LdsIO<F>, LdsPsi<F>, NoNeed, 1, 2, NT, true>(cur, cnt, tw, NoNeed{}, lio, psi);
-                else lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 1, 2, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
-                lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 2, NP - 1, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
+                if constexpr (LOGM >= 10) {
+                    if (nff == 2) lds_transform<F, true, LOGM, LdsIO<F>, LdsPsi<F>, NoNeed, 1, 2, NT, true>(cur, cnt, tw, NoNeed{}, lio, psi);
+                    else if (nff == 3) lds_transform<F, true, LOGM, LdsIO<F>, LdsIO<F>, NoNeed, 1, 2, NT>(cur, cnt, tw, NoNeed{}, lio, lio);
+                    else lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 1, 2, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
+                    if (nff == 3) lds_transform<F, true, LOGM, LdsIO<F>, LdsPsi<F>, NoNeed, 2, 3, NT, true>(cur, cnt, tw, NoNeed{}, lio, psi);
+                    else lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 2, 3, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
+                    lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 3, NP - 1, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
+                } else {
+                    if (nff == 2) lds_transform<F, true, LOGM, LdsIO<F>, LdsPsi<F>, NoNeed, 1, 2, NT, true>(cur, cnt, tw, NoNeed{}, lio, psi);
+                    else lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 1, 2, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
+                    lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 2, NP - 1, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
+                }
             } else {
                 lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, NP - 1, NT>(cur, cnt, tw, NoNeed{}, in, lio);
             }
@@ -1686,8 +1711,18 @@ __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_
             }
         }
         __syncthreads();
-        lds_transform<FT, false, LOGM, LdsIO<FT>, ParityOut, NoNeed, 1, 32, NT>(cur, a.p, twf, NoNeed{}, LdsIO<FT>{cur},
-                                                                         ParityOut{a, soff, tile, uo, &bad});
+        if constexpr (SUB && LOGM > 8) {
+            // FFT passes [1, FEND) in subfield coordinates, the last one writing
+            // normal coordinates back, then the full-field passes
+            constexpr int FEND = big_sub_fft_end(LOGM);
+            lds_transform<FT, false, LOGM, LdsIO<FT>, LdsPsi<F>, NoNeed, 1, FEND, NT, true>(
+                cur, a.p, twf, NoNeed{}, LdsIO<FT>{cur}, LdsPsi<F>{cur, a.tw_dmap});
+            lds_transform<F, false, LOGM, LdsIO<F>, ParityOutFull, NoNeed, FEND, 32, NT>(
+                cur, a.p, a.tw_fft, NoNeed{}, LdsIO<F>{cur}, ParityOutFull{a, soff, tile, uo, &bad});
+        } else {
+            lds_transform<FT, false, LOGM, LdsIO<FT>, ParityOut, NoNeed, 1, 32, NT>(cur, a.p, twf, NoNeed{}, LdsIO<FT>{cur},
+                                                                             ParityOut{a, soff, tile, uo, &bad});
+        }
         if constexpr (VERIFY) flag_mismatch(a.mismatch, bad != 0);
         return;
     }

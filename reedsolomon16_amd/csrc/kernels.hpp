@@ -36,6 +36,7 @@ struct EncodeArgs {
     // an element of GF(2^8) (leopard16.go:218-221), so the transform runs on
     // (lo ^ D(hi), hi) with kTwDwords8 subfield tables (6 v_perm_b32 per product
     // instead of 12); tw_dmap is the byte map D (make_sub_dmap).  nullptr: full field.
+    // m = 1024: the FFT passes before big_sub_fft_end(10) only (zero tables after them).
     const uint32_t *tw_fft_sub;
     const uint32_t *tw_dmap;
     // Optional (with tw_fft_sub): chunk c's IFFT passes from ifft_nff[c] on in
