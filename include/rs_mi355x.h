@@ -304,7 +304,7 @@ int rs_debug_zc_rows(uint8_t *const *rows, int nrows, size_t S);
  *   "rec_half" 0/1    GF(2^16) reconstruct with n = 1024 / 2048 in 32-byte half tiles, two
  *                     workgroups per CU (1), or 64-byte tiles, one per CU (0),
  *   "dec_lab" 0..255  schedule variants of the bit-sliced n = 256 decoder (0: the product),
- *   "lds_big" 0/1     GF(2^16) encode with m = 512 .. 2048 and reconstruct with n = 4096 / 8192 in one
+ *   "lds_big" 0/1     GF(2^16) encode with m = 512 .. 4096 and reconstruct with n = 4096 / 8192 in one
  *                     LDS-resident launch (1, default) or the multi-pass kernels (0),
  *   "zc"      0..3    host reconstruct over pinned mapped rows: zero-copy kernels move the
  *                     present rows in (bit 0) and the rebuilt rows out (bit 1) (default 3);

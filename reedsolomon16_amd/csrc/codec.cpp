@@ -363,7 +363,8 @@ bool rs::rec_half_enabled() { return g_path_rec_half.load(std::memory_order_rela
 namespace {
 
 // One LDS-resident encode launch covers m <= 256 (both fields) and, for
-// GF(2^16), m up to 2048 (64-byte tiles, half tiles at 2048, kernels.hpp kMaxLdsEncLogM16);
+// GF(2^16), m up to 4096 (64-byte tiles, half tiles at 2048, quarter tiles at
+// 4096, kernels.hpp kMaxLdsEncLogM16);
 // larger m runs the multi-pass kernels.
 bool enc_lds_ok(const rs_codec *c) {
     return c->logm <= kMaxLdsLogN ||

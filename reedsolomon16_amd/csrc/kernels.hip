@@ -1561,9 +1561,10 @@ __global__ void __launch_bounds__((rec_threads<LOGN, PKV>()), (PKV == 2 && LOGN 
 // m = 512, 1024 (GF(2^16), round 6): 64-byte tiles (F16<2>) and one
 // 1024-thread workgroup per CU, the m x 80-byte image(s) taking 80 KB of LDS
 // (m = 1024: acc in registers, one image; m = 512: acc and chunk images);
-// m = 2048: 32-byte half tiles (LTile PK = 2), acc and chunk images 128 KB.
+// m = 2048: 32-byte half tiles (LTile PK = 2), acc and chunk images 128 KB;
+// m = 4096: 16-byte quarter tiles (PK = 4), acc in registers, the image 64 KB.
 template <int LOGM> constexpr int enc_threads() { return LOGM >= 9 ? 1024 : 256; }
-template <int LOGM> constexpr int enc_pk() { return LOGM >= 11 ? 2 : 0; }
+template <int LOGM> constexpr int enc_pk() { return LOGM >= 12 ? 4 : LOGM >= 11 ? 2 : 0; }
 template <class F, int LOGM, bool VERIFY, class FT = F, bool ISUB = false>
 __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_enc_lds(EncodeArgs a) {
     constexpr int PK = enc_pk<LOGM>();
@@ -1574,13 +1575,14 @@ __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_
     constexpr bool ACCR = enc_acc_regs(LOGM);
     uint8_t *acc = lds_dyn, *cur = ACCR ? lds_dyn : lds_dyn + M * L::ROW;
     uint32_t bx = blockIdx.x;
-    if constexpr (PK == 2) {
-        // half tiles: the four tiles of a 128-byte line go to one XCD (as k_rec_lds)
-        if (bx < (gridDim.x & ~31u)) bx = (bx & ~31u) | ((bx & 7u) << 2) | ((bx >> 3) & 3u);
+    if constexpr (PK >= 2) {
+        // half (quarter) tiles: the 2 PK tiles of a 128-byte line go to one XCD (as k_rec_lds)
+        constexpr uint32_t T = 2 * PK, G = 8 * T;
+        if (bx < (gridDim.x & ~(G - 1))) bx = (bx & ~(G - 1)) | ((bx & 7u) * T) | ((bx >> 3) & (T - 1));
     }
-    // a half tile is addressed from its 64-byte block, its units from uo on
-    const uint64_t tile = PK == 2 ? (uint64_t)(bx >> 1) * 64 : (uint64_t)bx * L::TB;
-    const int uo = PK == 2 ? L::U * (int)(bx & 1u) : 0;
+    // a half (quarter) tile is addressed from its 64-byte block, its units from uo on
+    const uint64_t tile = PK >= 2 ? (uint64_t)(bx / PK) * 64 : (uint64_t)bx * L::TB;
+    const int uo = PK >= 2 ? L::U * (int)(bx % PK) : 0;
     const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
     constexpr int its = ifft_slot_count(LOGM);
     struct ChunkIn {
@@ -1651,30 +1653,30 @@ __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_
             const int row0 = c * M, cnt = a.k - row0 < M ? a.k - row0 : M;
             const uint32_t *tw = a.tw_ifft + (uint64_t)c * its * F::TWD;
             const uint32_t *tws = isub ? a.tw_ifft_sub + (uint64_t)c * its * FT::TWD : nullptr;
-            const LdsIO<F> lio{cur};
+            const LdsIO<F, PK> lio{cur};
             const ChunkIn in{a, row0, cnt, soff, tile, uo};
             if constexpr (isub) {
                 // full-field passes, the last one writing subfield coordinates, then subfield passes
-                const LdsPsi<F> psi{cur, a.tw_dmap};
-                const LdsIO<FT> lios{cur};
+                const LdsPsi<F, PK> psi{cur, a.tw_dmap};
+                const LdsIO<FT, PK> lios{cur};
                 // 1 or 2, and up to 3 for m = 1024 (codec.cpp upload_ifft_sub)
                 const int nff = a.ifft_nff[c];
-                if (nff == 1) lds_transform<F, true, LOGM, ChunkIn, LdsPsi<F>, NoNeed, 0, 1, NT, true>(cur, cnt, tw, NoNeed{}, in, psi);
-                else lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, 1, NT>(cur, cnt, tw, NoNeed{}, in, lio);
+                if (nff == 1) lds_transform<F, true, LOGM, ChunkIn, LdsPsi<F, PK>, NoNeed, 0, 1, NT, true, PK>(cur, cnt, tw, NoNeed{}, in, psi);
+                else lds_transform<F, true, LOGM, ChunkIn, LdsIO<F, PK>, NoNeed, 0, 1, NT, false, PK>(cur, cnt, tw, NoNeed{}, in, lio);
                 if constexpr (LOGM >= 10) {
-                    if (nff == 2) lds_transform<F, true, LOGM, LdsIO<F>, LdsPsi<F>, NoNeed, 1, 2, NT, true>(cur, cnt, tw, NoNeed{}, lio, psi);
-                    else if (nff == 3) lds_transform<F, true, LOGM, LdsIO<F>, LdsIO<F>, NoNeed, 1, 2, NT>(cur, cnt, tw, NoNeed{}, lio, lio);
-                    else lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 1, 2, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
-                    if (nff == 3) lds_transform<F, true, LOGM, LdsIO<F>, LdsPsi<F>, NoNeed, 2, 3, NT, true>(cur, cnt, tw, NoNeed{}, lio, psi);
-                    else lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 2, 3, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
-                    lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 3, NP - 1, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
+                    if (nff == 2) lds_transform<F, true, LOGM, LdsIO<F, PK>, LdsPsi<F, PK>, NoNeed, 1, 2, NT, true, PK>(cur, cnt, tw, NoNeed{}, lio, psi);
+                    else if (nff == 3) lds_transform<F, true, LOGM, LdsIO<F, PK>, LdsIO<F, PK>, NoNeed, 1, 2, NT, false, PK>(cur, cnt, tw, NoNeed{}, lio, lio);
+                    else lds_transform<FT, true, LOGM, LdsIO<FT, PK>, LdsIO<FT, PK>, NoNeed, 1, 2, NT, false, PK>(cur, cnt, tws, NoNeed{}, lios, lios);
+                    if (nff == 3) lds_transform<F, true, LOGM, LdsIO<F, PK>, LdsPsi<F, PK>, NoNeed, 2, 3, NT, true, PK>(cur, cnt, tw, NoNeed{}, lio, psi);
+                    else lds_transform<FT, true, LOGM, LdsIO<FT, PK>, LdsIO<FT, PK>, NoNeed, 2, 3, NT, false, PK>(cur, cnt, tws, NoNeed{}, lios, lios);
+                    lds_transform<FT, true, LOGM, LdsIO<FT, PK>, LdsIO<FT, PK>, NoNeed, 3, NP - 1, NT, false, PK>(cur, cnt, tws, NoNeed{}, lios, lios);
                 } else {
-                    if (nff == 2) lds_transform<F, true, LOGM, LdsIO<F>, LdsPsi<F>, NoNeed, 1, 2, NT, true>(cur, cnt, tw, NoNeed{}, lio, psi);
-                    else lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 1, 2, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
-                    lds_transform<FT, true, LOGM, LdsIO<FT>, LdsIO<FT>, NoNeed, 2, NP - 1, NT>(cur, cnt, tws, NoNeed{}, lios, lios);
+                    if (nff == 2) lds_transform<F, true, LOGM, LdsIO<F, PK>, LdsPsi<F, PK>, NoNeed, 1, 2, NT, true, PK>(cur, cnt, tw, NoNeed{}, lio, psi);
+                    else lds_transform<FT, true, LOGM, LdsIO<FT, PK>, LdsIO<FT, PK>, NoNeed, 1, 2, NT, false, PK>(cur, cnt, tws, NoNeed{}, lios, lios);
+                    lds_transform<FT, true, LOGM, LdsIO<FT, PK>, LdsIO<FT, PK>, NoNeed, 2, NP - 1, NT, false, PK>(cur, cnt, tws, NoNeed{}, lios, lios);
                 }
             } else {
-                lds_transform<F, true, LOGM, ChunkIn, LdsIO<F>, NoNeed, 0, NP - 1, NT>(cur, cnt, tw, NoNeed{}, in, lio);
+                lds_transform<F, true, LOGM, ChunkIn, LdsIO<F, PK>, NoNeed, 0, NP - 1, NT, false, PK>(cur, cnt, tw, NoNeed{}, in, lio);
             }
 #pragma unroll
             for (int k = 0; k < KF; k++) {
@@ -1715,12 +1717,12 @@ __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_
             // FFT passes [1, FEND) in subfield coordinates, the last one writing
             // normal coordinates back, then the full-field passes
             constexpr int FEND = big_sub_fft_end(LOGM);
-            lds_transform<FT, false, LOGM, LdsIO<FT>, LdsPsi<F>, NoNeed, 1, FEND, NT, true>(
-                cur, a.p, twf, NoNeed{}, LdsIO<FT>{cur}, LdsPsi<F>{cur, a.tw_dmap});
-            lds_transform<F, false, LOGM, LdsIO<F>, ParityOutFull, NoNeed, FEND, 32, NT>(
-                cur, a.p, a.tw_fft, NoNeed{}, LdsIO<F>{cur}, ParityOutFull{a, soff, tile, uo, &bad});
+            lds_transform<FT, false, LOGM, LdsIO<FT, PK>, LdsPsi<F, PK>, NoNeed, 1, FEND, NT, true, PK>(
+                cur, a.p, twf, NoNeed{}, LdsIO<FT, PK>{cur}, LdsPsi<F, PK>{cur, a.tw_dmap});
+            lds_transform<F, false, LOGM, LdsIO<F, PK>, ParityOutFull, NoNeed, FEND, 32, NT, false, PK>(
+                cur, a.p, a.tw_fft, NoNeed{}, LdsIO<F, PK>{cur}, ParityOutFull{a, soff, tile, uo, &bad});
         } else {
-            lds_transform<FT, false, LOGM, LdsIO<FT>, ParityOut, NoNeed, 1, 32, NT>(cur, a.p, twf, NoNeed{}, LdsIO<FT>{cur},
+            lds_transform<FT, false, LOGM, LdsIO<FT, PK>, ParityOut, NoNeed, 1, 32, NT, false, PK>(cur, a.p, twf, NoNeed{}, LdsIO<FT, PK>{cur},
                                                                              ParityOut{a, soff, tile, uo, &bad});
         }
         if constexpr (VERIFY) flag_mismatch(a.mismatch, bad != 0);
@@ -1852,11 +1854,12 @@ hipError_t enc_lds_f(int logm, bool verify, const EncodeArgs &a, hipStream_t s) 
         case 7: return enc_lds_t<F, 7>(verify, a, s);
         case 8: return enc_lds_t<F, 8>(verify, a, s);
     }
-    if constexpr (std::is_same<F, F16<2>>::value) {  // m = 512, 1024: 64-byte tiles; 2048: half tiles
+    if constexpr (std::is_same<F, F16<2>>::value) {  // m = 512, 1024: 64-byte tiles; 2048: half, 4096: quarter tiles
         switch (logm) {
             case 9: return enc_lds_t<F, 9>(verify, a, s);
             case 10: return enc_lds_t<F, 10>(verify, a, s);
             case 11: return enc_lds_t<F, 11>(verify, a, s);
+            case 12: return enc_lds_t<F, 12>(verify, a, s);
         }
     }
     return hipErrorInvalidValue;

@@ -36,7 +36,7 @@ struct EncodeArgs {
     // an element of GF(2^8) (leopard16.go:218-221), so the transform runs on
     // (lo ^ D(hi), hi) with kTwDwords8 subfield tables (6 v_perm_b32 per product
     // instead of 12); tw_dmap is the byte map D (make_sub_dmap).  nullptr: full field.
-    // m = 1024: the FFT passes before big_sub_fft_end(10) only (zero tables after them).
+    // m = 1024, 4096: the FFT passes before big_sub_fft_end only (zero tables after them).
     const uint32_t *tw_fft_sub;
     const uint32_t *tw_dmap;
     // Optional (with tw_fft_sub): chunk c's IFFT passes from ifft_nff[c] on in
@@ -164,8 +164,9 @@ hipError_t launch_rec_lds(int bits, int logn, bool sub, const RecArgs &a, hipStr
 bool rec_bs256_available(int bits, int logn, bool sub, int mtrunc);
 hipError_t launch_rec_bs256(const RecArgs &a, hipStream_t s);
 // Encode (or verify) for 2 <= logm <= 8, and GF(2^16) up to kMaxLdsEncLogM16
-// (64-byte tiles, 32-byte half tiles at m = 2048), twiddles as for launch_encode_reg.
-constexpr int kMaxLdsEncLogM16 = 11;
+// (64-byte tiles, 32-byte half tiles at m = 2048, 16-byte quarter tiles at
+// m = 4096), twiddles as for launch_encode_reg.
+constexpr int kMaxLdsEncLogM16 = 12;
 hipError_t launch_encode_lds(int bits, int logm, bool verify, const EncodeArgs &a, hipStream_t s);
 
 

@@ -140,11 +140,13 @@ def test_constructor_errors():
     assert rs.New16(10, 1).encode_path == "reg16-m1"
     assert rs.New16(1024, 256).encode_path == "lds-m256"
     assert rs.New16(96, 100).encode_path == "lds-m128"
-    # m = 512 .. 2048 (GF(2^16)): the LDS encode (64-byte tiles, half tiles at 2048); m = 4096: multi-pass
+    # m = 512 .. 4096 (GF(2^16)): the LDS encode (64-byte tiles, half tiles at 2048, quarter
+    # tiles at 4096); m = 8192: multi-pass
     assert rs.New16(1024, 300).encode_path == "lds-m512"
     assert rs.New16(4000, 1000).encode_path == "lds-m1024"
     assert rs.New16(3000, 1025).encode_path == "lds-m2048"
-    assert rs.New16(3000, 2049).encode_path == "multipass"
+    assert rs.New16(3000, 2049).encode_path == "lds-m4096"
+    assert rs.New16(1000, 5000).encode_path == "multipass"
 
 
 def test_debug_set_path_knobs(paths):

@@ -1,6 +1,6 @@
-"""The LDS-resident encode for m = 512 .. 2048 (GF(2^16), kernels.hip
-k_enc_lds with 64-byte tiles, 32-byte half tiles at m = 2048, and 1024
-threads): bit-exact against the oracle
+"""The LDS-resident encode for m = 512 .. 4096 (GF(2^16), kernels.hip
+k_enc_lds with 64-byte tiles, 32-byte half tiles at m = 2048, 16-byte quarter
+tiles at m = 4096, and 1024 threads): bit-exact against the oracle
 on ragged geometries, batched / table / host-pipeline row layouts, verify, and
 the reference's own large-shard-count tests replayed end to end
 (reedsolomon_test.go:61-84 "500 / 1000 / 5000 Shards": testEncodeDecode
@@ -31,7 +31,7 @@ def rand_data(rng, k, S):
 # p < m and p a power of two, one and several 64-byte blocks
 GEOMS = [(300, 300, 64), (700, 300, 128), (512, 512, 192), (1100, 257, 64), (4000, 1000, 64),
          (1000, 600, 128), (2047, 1024, 64), (600, 700, 64 * 5), (3000, 1025, 64), (2048, 2048, 128),
-         (5000, 1500, 64 * 3)]
+         (5000, 1500, 64 * 3), (3000, 2049, 64), (5000, 4096, 128)]
 
 
 @pytest.mark.parametrize("k,p,S", GEOMS)
@@ -52,7 +52,8 @@ def test_encode_matches_oracle(k, p, S):
     assert not c.verify(shards)
 
 
-@pytest.mark.parametrize("k,p,S,B", [(700, 300, 4096 + 64, 3), (3000, 1000, 256, 2)])
+@pytest.mark.parametrize("k,p,S,B", [(700, 300, 4096 + 64, 3), (3000, 1000, 256, 2), (3000, 1500, 64 * 3, 2),
+                                     (2000, 4000, 64 * 3, 2)])
 def test_device_batch_and_table(torch, k, p, S, B):
     """Strided stripes in one launch (grid.y), and the same stripe through a row table."""
     rng = np.random.default_rng(k + p + B)
@@ -143,9 +144,9 @@ def test_reference_large_shard_count_5000():
     assert buf.getvalue() == data.tobytes()
 
 
-def test_m4096_stays_multipass():
-    """m = 4096 (p > 2048) keeps the multi-pass encode; still oracle-exact."""
-    k, p, S = 1500, 2100, 64
+def test_m8192_stays_multipass():
+    """m = 8192 (p > 4096) keeps the multi-pass encode; still oracle-exact."""
+    k, p, S = 1500, 4100, 64
     rng = np.random.default_rng(2048)
     data = rand_data(rng, k, S)
     c = rs.New16(k, p)
@@ -155,7 +156,7 @@ def test_m4096_stays_multipass():
     assert np.array_equal(np.stack(shards[k:]), orc.encode(16, k, p, data))
 
 
-@pytest.mark.parametrize("k,p,S", [(700, 300, 4096 + 64), (2500, 1000, 512), (3000, 1500, 64 * 7)])
+@pytest.mark.parametrize("k,p,S", [(700, 300, 4096 + 64), (2500, 1000, 512), (3000, 1500, 64 * 7), (3000, 3000, 64 * 5)])
 def test_lds_equals_multipass(torch, paths, k, p, S):
     """The one-launch LDS encode and the multi-pass kernels (rs_debug_set_path
     "lds_big" 0) write identical parity, two stripes per launch."""

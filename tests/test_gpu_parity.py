@@ -1065,13 +1065,16 @@ def test_verify_and_reconstruct_async_stream_of_blocks(k, p, S):
 
 
 @pytest.mark.parametrize("k,p,S", [(1024, 256, 1024), (300, 200, 512), (100, 40, 256), (1000, 129, 128),
-                                   (4000, 1000, 256), (3500, 600, 128), (1500, 1024, 64 * 3)])
+                                   (4000, 1000, 256), (3500, 600, 128), (1500, 1024, 64 * 3),
+                                   (2000, 3000, 128), (13000, 2100, 64)])
 def test_lds_encode_subfield_chunk_passes(torch_dev, paths, k, p, S):
     """k_enc_lds with the chunk IFFTs in subfield coordinates from their first
     all-subfield pass on (EncodeArgs::tw_ifft_sub, default) and the full-field
     chunk IFFTs (rs_debug_set_path("sub", 0)) both give the oracle's parity, and verify it.
-    m = 1024 (round 6): chunk passes full-field up to pass 1, 2 or 3 (chunk 3:
-    layers 0-4) and the FFT's last pass full-field."""
+    m = 1024, 4096 (round 6): chunk passes full-field up to pass 1, 2 or 3 (m = 1024
+    chunk 3: layers 0-4) and the FFT's last passes full-field; at m = 4096 a
+    fourth chunk (layers 0-6 full-field) keeps every chunk full-field and only
+    the FFT in subfield coordinates."""
     torch = torch_dev
     rng = np.random.default_rng(k + p + S)
     data = rand_data(rng, k, S)

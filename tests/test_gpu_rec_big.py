@@ -85,10 +85,10 @@ def test_big_n_reconstruct_dev_equals_oracle(torch, k, p, S, pattern):
                 assert not got[i].any(), (pattern, recover_all, i)
 
 
-def test_big_n_row_list_and_batch(torch):
+@pytest.mark.parametrize("k,p,S,ns", [(1024, 256, 256, 3), (3000, 1000, 128, 2), (4000, 1000, 64, 2)])
+def test_big_n_row_list_and_batch(torch, k, p, S, ns):
     """Row pointers that are not equally strided (the ring-slot launch), then
-    three stripes at padded row / stripe strides in one launch."""
-    k, p, S, ns = 1024, 256, 256, 3
+    several stripes at padded row / stripe strides in one launch (n = 2048, 4096, 8192)."""
     full = encoded(k, p, S, 5)
     er = patterns(k, p, 6)["random_p"]
     mask = np.zeros(k + p, bool)
