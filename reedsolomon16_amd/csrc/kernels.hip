@@ -1581,8 +1581,9 @@ __global__ void __launch_bounds__((enc_threads<LOGM>()), (LOGM >= 9 ? 1 : 4)) k_
         if (bx < (gridDim.x & ~(G - 1))) bx = (bx & ~(G - 1)) | ((bx & 7u) * T) | ((bx >> 3) & (T - 1));
     }
     // a half (quarter) tile is addressed from its 64-byte block, its units from uo on
-    const uint64_t tile = PK >= 2 ? (uint64_t)(bx / PK) * 64 : (uint64_t)bx * L::TB;
-    const int uo = PK >= 2 ? L::U * (int)(bx % PK) : 0;
+    constexpr uint32_t PD = PK >= 2 ? PK : 1;  // tiles per 64-byte block
+    const uint64_t tile = PK >= 2 ? (uint64_t)(bx / PD) * 64 : (uint64_t)bx * L::TB;
+    const int uo = PK >= 2 ? L::U * (int)(bx % PD) : 0;
     const uint64_t soff = (uint64_t)blockIdx.y * a.stripe_stride;
     constexpr int its = ifft_slot_count(LOGM);
     struct ChunkIn {

@@ -43,6 +43,8 @@ CONFIGS = {
     "L1024v": (16, 4000, 1000, 64 << 10, "verify"),
     "L2048": (16, 3000, 1500, 64 << 10, "encode"),
     "L4096": (16, 3000, 3000, 64 << 10, "encode"),
+    "L512v": (16, 700, 300, 256 << 10, "verify"),
+    "L2048v": (16, 3000, 1500, 64 << 10, "verify"),
     # n = 4096 reconstruct (3000 + 1000: 1000 erasures; 2100 + 10: 10 erasures)
     "R4096": (16, 3000, 1000, 64 << 10, "reconstruct"),
     "R4096e10": (16, 2100, 10, 256 << 10, "reconstruct"),
