@@ -16,14 +16,20 @@ every rank checks WORLD_SIZE == --gpus.  Started directly with --gpus N > 1,
 the parent launches `python -m torch.distributed.run --nproc-per-node N` on
 this same command line before it imports torch or touches a GPU, and exits
 with the child's return code.  --dry-run runs the rank layout with gloo on the
-CPU (no GPU): each rank reports its byte range.
-  --split bytes   (default) the north-star layout: rank r owns the byte range
-                  dist.byte_range(S, r, N) of every shard of the same B stripes
-                  (column independence, leopard16.go:778-792) and encodes it;
-                  no collective on the data path.  Total work is fixed as N
-                  grows -> "scaling": "strong"; value = B*k*S data bytes /
-                  max-over-ranks wall time.
-  --split stripes each rank encodes B stripes of its own -> "weak".
+CPU (no GPU): each rank reports its byte range.  Every layout runs without a
+collective on the data path (column independence, leopard16.go:778-792):
+  --split bytes-weak  (default, round 6) the north-star layout with the
+                  per-GPU work fixed: the job is N*B stripes and rank r owns
+                  the byte range dist.byte_range(S, r, N) of every shard of
+                  all of them, so each rank's launch moves the bytes of B
+                  whole stripes (N*B stripes x S/N bytes) as N grows ->
+                  "scaling": "weak"; value = N*B*k*S data bytes / max-over-
+                  ranks wall time.  At N = 1 it is the one-GPU line.
+  --split bytes   the same byte ranges of a fixed B stripes: total work fixed
+                  as N grows -> "strong" (each rank's launch shrinks N-fold;
+                  the 8-rank slice of 256 stripes runs 0.60-0.66 of the
+                  roofline against 0.67-0.69 at 2048 stripes).
+  --split stripes each rank encodes B whole stripes of its own -> "weak".
 
 Prints one JSON line (rank 0).  `roofline` is for the dominant (only) kernel:
 achieved = algorithmic bytes per launch ((k+p)*bytes-per-row: read k rows,
@@ -461,6 +467,17 @@ def launch_ranks(n: int) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def rank_stripes(args, world: int) -> int:
+    """Stripes in one rank's launch: the byte range of N*B stripes (bytes-weak,
+    and --slice-of N: the launch shape of one of its ranks), else B."""
+    n = args.slice_of if args.slice_of > 1 else world
+    return args.stripes * n if args.split == "bytes-weak" else args.stripes
+
+
+def scaling_of(args) -> str:
+    return "strong" if args.split == "bytes" else "weak"
+
+
 def dry_run(args, rank: int, world: int) -> None:
     """The rank layout without a GPU: gloo process group, each rank's byte
     range of the workload's shards, gathered on rank 0 and printed as JSON."""
@@ -473,16 +490,18 @@ def dry_run(args, rank: int, world: int) -> None:
     else:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
     K, P, S = WORKLOADS[args.workload]
-    lo, hi = rsd.byte_range(S, rank, world) if args.split == "bytes" else (0, S)
+    lo, hi = rsd.byte_range(S, rank, world) if args.split != "stripes" else (0, S)
+    br = rank_stripes(args, world)
     kname = "bs16-m32" if args.workload == "C3" else "lds-m256"  # the engine's path for the workload (rs_encode_path)
     got = [None] * world
     dist.all_gather_object(got, {"rank": rank, "byte_range": [lo, hi], "world": dist.get_world_size(),
-                                 "traffic_key": traffic_key(args.workload, kname, args.stripes, hi - lo),
-                                 "traffic": load_traffic(kname, args.workload, args.stripes, hi - lo, S)})
+                                 "stripes_per_launch": br,
+                                 "traffic_key": traffic_key(args.workload, kname, br, hi - lo),
+                                 "traffic": load_traffic(kname, args.workload, br, hi - lo, S)})
     if rank == 0:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_requested": args.gpus, "workload": args.workload,
-                          "split": args.split, "ranks": got,
+                          "split": args.split, "scaling": scaling_of(args), "ranks": got,
                           # the evidence keys of a real N-rank line (kernel times need a GPU)
                           "roofline": {"traffic": got[0]["traffic"], "traffic_key": got[0]["traffic_key"],
                                        "per_rank_traffic": [r["traffic"] for r in got]},
@@ -499,8 +518,9 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="C3")
-    ap.add_argument("--split", choices=["bytes", "stripes"], default="bytes",
-                    help="multi-GPU layout: byte ranges of the same stripes (strong) or own stripes (weak)")
+    ap.add_argument("--split", choices=["bytes-weak", "bytes", "stripes"], default="bytes-weak",
+                    help="multi-GPU layout: byte ranges of N x --stripes stripes (weak, default), byte ranges of "
+                         "--stripes stripes (strong), or whole stripes per rank (weak)")
     ap.add_argument("--stripes", type=int, default=256, help="stripes encoded per step (one launch per rank)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
@@ -543,12 +563,12 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     K, P, S = WORKLOADS[args.workload]
-    B = args.stripes
+    B = rank_stripes(args, world)  # stripes in this rank's launch
     if args.slice_of > 1:
         if world != 1:
             raise SystemExit("--slice-of is a one-GPU measurement")
         lo, hi = rsd.byte_range(S, 0, args.slice_of)
-    elif args.split == "bytes":
+    elif args.split != "stripes":
         lo, hi = rsd.byte_range(S, rank, world)
     else:
         lo, hi = 0, S
@@ -628,7 +648,7 @@ def main():
         host = host_resident(rs)
 
     ms_per_step = el / args.steps * 1e3
-    job_stripes = B if args.split == "bytes" else world * B
+    job_stripes = B if args.split != "stripes" else world * B  # stripes the whole job encodes per step
     data_bytes = args.steps * job_stripes * K * S
     value = data_bytes / el / 2**30
     alg_bytes = B * (K + P) * W  # per launch on one rank
@@ -648,21 +668,23 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "strong" if args.split == "bytes" else "weak",
+            "scaling": scaling_of(args),
             "vs_baseline": None,
             "dtype": "u8 (GF(2^16) symbols)",
             "data": "synthetic (uniform random bytes, torch.randint seed 0x5EED+rank)",
             "config": {
                 "workload": f"{args.workload}: GF(2^16) Leopard encode, {K} data + {P} parity shards x {S >> 10} KiB, "
-                            f"{B} stripes per step (one launch per rank)",
-                "stripes_per_step": B,
+                            f"{job_stripes} stripes per step (one launch per rank)",
+                "stripes_per_step": job_stripes,
+                "stripes_per_rank_launch": B,
                 "data_shards": K,
                 "parity_shards": P,
                 "shard_bytes": S,
                 "parallelism": (f"one GPU running rank 0's slice of a {args.slice_of}-rank byte-range split: {W} bytes of every row"
                                 if args.slice_of > 1 else
                                 f"byte-range split over {world} rank(s): {W} bytes of every row per rank"
-                                if args.split == "bytes" else f"independent stripes, {world} rank(s)"),
+                                + (" (per-rank work fixed: the job grows with N)" if args.split == "bytes-weak" and world > 1 else "")
+                                if args.split != "stripes" else f"independent stripes, {world} rank(s)"),
                 "row_bytes_per_rank": W,
                 "kernel_path": kname,
                 "layout": f"rows at a stride of {W} + {pad} bytes, stripes back to back",

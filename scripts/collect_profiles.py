@@ -46,8 +46,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", type=int, required=True)
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out", "round"))
+    ap.add_argument("--suffix", default="", help="file-name suffix (a second evidence set of the same round)")
     a = ap.parse_args()
-    tag = f"r{a.round:02d}"
+    tag = f"r{a.round:02d}{a.suffix}"
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
 
@@ -75,10 +76,19 @@ def main():
     stripes = bench["config"].get("stripes_per_step", 16)
     workload = bench["config"]["workload"].split(":")[0]
     agg = collections.defaultdict(list)
+    nstr = {}  # row slice -> stripes per launch of that pass (its bench line, when it has one)
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         for d in glob.glob(os.path.join(a.src, f"pmc_{c}*")):
+            if not os.path.isdir(d):
+                continue
             m = re.search(r"_s(\d+)$", d)
             W = byte_range(S, 0, int(m.group(1)))[1] if m else bench["config"].get("row_bytes_per_rank", S)
+            try:  # bench.py --slice-of N in the bytes-weak layout launches N x stripes
+                with open(d + ".json") as f:
+                    cfg = json.loads([l for l in f if l.startswith("{")][-1])["config"]
+                nstr[W] = cfg.get("stripes_per_rank_launch", cfg.get("stripes_per_step", stripes))
+            except (OSError, IndexError, ValueError, KeyError):
+                nstr.setdefault(W, stripes)
             for fn in glob.glob(os.path.join(d, "run_counter_collection.csv")):
                 for r in csv.DictReader(open(fn)):
                     p = path_of(r["Kernel_Name"])
@@ -86,6 +96,7 @@ def main():
                         agg[(p, W, r["Counter_Name"])].append(float(r["Counter_Value"]))
     traffic, lines = {}, []
     for p, W in sorted({k[:2] for k in agg}):
+        stripes_w = nstr.get(W, stripes)
         fk = agg.get((p, W, "FETCH_SIZE"), [])
         wk = agg.get((p, W, "WRITE_SIZE"), [])
         if not fk or not wk:
@@ -93,14 +104,14 @@ def main():
         fetch = sum(fk) / len(fk) * 1024
         write = sum(wk) / len(wk) * 1024
         hbm = 2 * fetch + write
-        alg = stripes * (bench["config"]["data_shards"] + bench["config"]["parity_shards"]) * W
-        traffic[f"{workload}:{p}:{stripes}x{W}"] = {
+        alg = stripes_w * (bench["config"]["data_shards"] + bench["config"]["parity_shards"]) * W
+        traffic[f"{workload}:{p}:{stripes_w}x{W}"] = {
             "hbm_bytes_per_launch": round(hbm), "fetch_size_bytes": round(fetch),
-            "write_size_bytes": round(write), "launches": len(fk), "stripes": stripes, "row_bytes": W,
+            "write_size_bytes": round(write), "launches": len(fk), "stripes": stripes_w, "row_bytes": W,
             "alg_bytes_per_launch": alg, "traffic_over_alg": round(hbm / alg, 4),
             "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE = half of streamed reads)",
             "round": tag}
-        lines.append(f"{p} {stripes}x{W}: FETCH_SIZE {fetch/1e6:.2f} MB (x2 = {2*fetch/1e6:.2f}), WRITE_SIZE "
+        lines.append(f"{p} {stripes_w}x{W}: FETCH_SIZE {fetch/1e6:.2f} MB (x2 = {2*fetch/1e6:.2f}), WRITE_SIZE "
                      f"{write/1e6:.2f} MB, HBM {hbm/1e6:.2f} MB/launch ({hbm/alg:.4f} x algorithmic) over {len(fk)} launches")
     kern = [r for r in rows if "k_enc" in r["Name"] or "k_rec" in r["Name"]]
     for r in kern:

@@ -24,6 +24,15 @@ for cfg in C4x16 C2 C2x16 C5b32 C5rb8; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$cfg -o run -- python3 scripts/time_ops.py --configs $cfg --iters 20 > $OUT/trace_$cfg.json 2> $OUT/trace_$cfg.err
   rc=$?; echo "trace $cfg rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
+# each rank's launch shape of an N-GPU run (bench.py --slice-of N, default
+# bytes-weak layout: rank 0's byte range of N x 256 stripes), and the strong
+# layout's 8-rank shape (256 stripes) beside it
+for n in 2 4 8; do
+  timeout -k 10 300 python bench.py --slice-of $n --no-cpu --no-other --no-host $BARGS > $OUT/slice_$n.json 2> $OUT/slice_$n.err
+  rc=$?; echo "slice $n rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+timeout -k 10 300 python bench.py --split bytes --slice-of 8 --no-cpu --no-other --no-host $BARGS > $OUT/slice_8_strong.json 2> $OUT/slice_8_strong.err
+rc=$?; echo "slice 8 strong rc=$rc"; [ $rc -eq 0 ] || exit $rc
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o run -- python3 bench.py --no-cpu --no-single --no-unpadded --no-other --no-host --steps 50 --warmup 5 > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc

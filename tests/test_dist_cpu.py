@@ -170,6 +170,10 @@ def test_bench_launcher_starts_n_ranks(gpus, workload):
     assert "traffic" in res["roofline"] and len(res["roofline"]["per_rank_traffic"]) == gpus
     for r in res["ranks"]:
         assert r["traffic_key"].endswith("x%d" % (r["byte_range"][1] - r["byte_range"][0]))
+        # the default layout keeps the per-GPU work fixed: each rank's launch
+        # covers its byte range of N x 256 stripes
+        assert r["stripes_per_launch"] == 256 * gpus
+    assert res["split"] == "bytes-weak" and res["scaling"] == "weak"
     assert len(res["per_rank_frac"]) == gpus
     cb = res["cpu_baseline"]
     assert cb["unit"] == "GiB/s" and cb["value"] > 0 and cb["kind"] == "port"
