@@ -42,6 +42,44 @@ def path_of(name: str):
     return None
 
 
+def rank_slices(src: str, out: str, bench: dict) -> None:
+    """Per-rank launch shapes (bench.py --slice-of N, gpu_round.sh slice_N.json
+    and slice_8_strong.json) beside the one-GPU line: kernel time, roofline
+    fraction and the job value an N-rank run would report if every rank ran at
+    that rate.  Written only when the round script produced the slices."""
+    lines = []
+
+    def one(label, d, n):
+        c, r = d["config"], d["roofline"]
+        job = d["value"]  # a --slice-of line already counts the whole job's shard bytes (k * S per stripe)
+        lines.append(f"{label:<28} W={c['row_bytes_per_rank']:>8}  stripes/launch {c['stripes_per_rank_launch']:>5}  "
+                     f"kernel {r['kernel_ms']:.4f} ms  frac {r['frac']:.4f}  projected job GiB/s {job:.1f}  "
+                     f"efficiency {r['frac'] / bench['roofline']['frac']:.3f}")
+
+    one("1 rank (the bench line)", bench, 1)
+    found = False
+    for n in (2, 4, 8):
+        p = os.path.join(src, f"slice_{n}.json")
+        if os.path.exists(p):
+            with open(p) as f:
+                one(f"{n}-rank slice (bytes-weak)", json.loads([l for l in f if l.startswith("{")][-1]), n)
+            found = True
+    p = os.path.join(src, "slice_8_strong.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            one("8-rank slice (strong)", json.loads([l for l in f if l.startswith("{")][-1]), 8)
+    if not found:
+        return
+    with open(out, "w") as f:
+        f.write("# Per-rank launch shapes of an N-GPU byte-range run on one GPU (bench.py --slice-of N, "
+                "scripts/gpu_round.sh), HIP events.\n# bytes-weak (the default): rank 0's byte range of N x "
+                f"{bench['config']['stripes_per_rank_launch']} stripes; strong: of {bench['config']['stripes_per_rank_launch']} stripes.\n"
+                "# efficiency = the slice's roofline fraction over the one-GPU line's (the kernel-only scaling "
+                "efficiency an N-GPU run would show if each GPU ran like this one).\n")
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", type=int, required=True)
@@ -56,6 +94,8 @@ def main():
         bench = json.loads([l for l in f if l.startswith("{")][-1])
     with open(os.path.join(prof, f"{tag}_bench.json"), "w") as f:
         json.dump(bench, f, indent=1)
+
+    rank_slices(a.src, os.path.join(prof, f"{tag}_rank_slices.txt"), bench)
 
     rows = list(csv.DictReader(open(os.path.join(a.src, "trace", "run_kernel_stats.csv"))))
     with open(os.path.join(prof, f"{tag}_kernel_stats.csv"), "w", newline="") as f:
