@@ -533,6 +533,9 @@ def main():
     ap.add_argument("--dry-run", action="store_true", help="rank layout only: gloo on the CPU, no GPU")
     ap.add_argument("--no-other", action="store_true", help="skip the C4 / C5 kernel figures (one GPU only)")
     ap.add_argument("--no-host", action="store_true", help="skip the host-resident (PCIe-inclusive) figures")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group of an N-rank run: nccl (RCCL, one GPU per rank, the product) or gloo "
+                         "(a rehearsal of the same rank code on fewer GPUs than ranks: rank r uses GPU r %% count)")
     ap.add_argument("--slice-of", type=int, default=0,
                     help="one GPU: encode rank 0's byte range of an N-rank split (the launch shape each rank of an "
                          "N-GPU run has, for its rocprofv3 PMC passes); not a job-throughput figure")
@@ -555,7 +558,10 @@ def main():
     import reedsolomon16_amd as rs
     from reedsolomon16_amd import dist as rsd
 
-    if world > 1:
+    if world > 1 and args.backend == "gloo":
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -591,9 +597,15 @@ def main():
     flat = buf[: B * (K + P) * W].view(B, K + P, W)
     stream = torch.cuda.current_stream()
 
+    def rank_barrier():
+        if args.backend == "gloo":
+            dist.barrier()
+        else:
+            dist.barrier(device_ids=[dev.index])
+
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[dev.index])
+            rank_barrier()
         torch.cuda.synchronize()
 
     def timed(view, steps):
@@ -721,14 +733,14 @@ def main():
                 "kernel_ms": round(one_ms, 5),
                 "frac": round((K + P) * W / (one_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
             },
-            # rank 0 only, after the timed region (the other ranks wait at the barrier below)
-            "cpu_baseline": None if args.no_cpu else cpu_baseline(K, P, S, args.cpu_seconds, threads),
+            # rank 0 of a one-GPU run only, after the timed region
+            "cpu_baseline": None if args.no_cpu or world > 1 else cpu_baseline(K, P, S, args.cpu_seconds, threads),
             "other_workloads": other,
             "host_resident": host,
         }
         print(json.dumps(res), flush=True)
     if world > 1:
-        dist.barrier(device_ids=[dev.index])
+        rank_barrier()
         dist.destroy_process_group()
 
 
